@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""Benchmark: batched cauchy_256 encode + decode, device-resident, on 1..8 MI355X GPUs.
+
+One step = encode a batch of code groups (k data -> m recovery blocks each) + decode the same
+number of groups with e erased originals each (read k received blocks, write e recovered ones),
+inputs already resident in HBM. Headline config (BASELINE.json metric): k=200, m=32, 1400-byte
+blocks, e = m = 32 (worst case), 8192 groups per GPU. Multi-GPU: one process per GPU, groups
+sharded with no data-path collective (independent units -> weak scaling); timing is bracketed by
+barrier + synchronize and the max over ranks is reported.
+
+value = algorithmic GiB/s over all ranks: encode moves (k+m)*B and decode (k+e)*B bytes per group
+(SURVEY.md §8d). roofline: the dominant op, timed with HIP events on the stream its kernels run
+on, against the 8 TB/s HBM3E peak. cpu_baseline: the reference codec (oracle/_ref, compiled from
+catid/shorthair) on the host cores, rank 0 only, bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--k", type=int, default=200)
+    p.add_argument("--m", type=int, default=32)
+    p.add_argument("--block", type=int, default=1400)
+    p.add_argument("--groups", type=int, default=8192, help="code groups per GPU per op")
+    p.add_argument("--erasures", type=int, default=32, help="erasures per decoded group (0=random 1..m)")
+    p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline sample wall time")
+    p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    p.add_argument("--no-cpu", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(k, m, B, e_fixed, seconds, threads):
+    """Reference codec (oracle/_ref/libref_cauchy.so) encode+decode on host threads.
+
+    Returns None when the reference build is absent. Each thread loops over a few distinct
+    groups (same synthetic generator as the GPU run) until `seconds` elapse.
+    """
+    try:
+        from oracle import pyoracle as po
+        ref = po.reference()
+    except Exception:
+        ref = None
+    kind = "reference"
+    if ref is None:
+        return None
+    ora = po.oracle()
+    nsample = 4
+    groups = []
+    for g in range(nsample):
+        data = po.fill_group(g, k, B, 0xBE)
+        _, rec = ora.encode(k, m, data, B)
+        e, rows = po.erasure_pattern(g, k, m, 0xBE, e_fixed)
+        whole = np.concatenate([data, rec])
+        groups.append((data, rows, whole, e))
+    counts = [0] * threads
+    bytes_done = [0] * threads
+    stop = time.perf_counter() + seconds
+
+    def work(t):
+        out = np.empty((m, B), np.uint8)
+        i = t
+        while time.perf_counter() < stop:
+            data, rows, whole, e = groups[i % nsample]
+            ref.encode(k, m, data, B, out)
+            blocks = [whole[r].copy() for r in rows]
+            ref.decode(k, m, blocks, [int(r) for r in rows], B)
+            counts[t] += 1
+            bytes_done[t] += (k + m) * B + (k + e) * B
+            i += threads
+
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    dt = time.perf_counter() - t0
+    return dict(value=round(sum(bytes_done) / dt / 2**30, 4), unit="GiB/s", cores=threads, kind=kind,
+                sample=f"{sum(counts)} encode+decode group pairs (k={k} m={m} B={B} e={e_fixed or 'rand'}) "
+                       f"over {dt:.1f}s on {threads} host threads, ctypes-released GIL, "
+                       f"reference built -O3 -march=x86-64-v3, gf256_init not called (as shipped)")
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    import shorthair_amd as sh
+    assert sh.lib.cauchy_256_batch_init(local if world > 1 else 0) == 0
+
+    k, m, B, G = args.k, args.m, args.block, args.groups
+    emax = min(k, m)
+    stream = torch.cuda.current_stream()
+    s = stream.cuda_stream
+
+    # ---- device-resident synthetic inputs (per rank: its own shard of groups) ----
+    g0 = rank * G
+    enc_in = torch.empty((G, k, B), dtype=torch.uint8, device="cuda")
+    enc_out = torch.empty((G, m, B), dtype=torch.uint8, device="cuda")
+    sh.fill_synthetic(enc_in, k, B, G, g0, 0xBE, s)
+    sh.encode_batch(k, m, B, G, enc_in, enc_out, s)
+    # decode input: each group with its erasure pattern (survivors then recovery rows)
+    from oracle import pyoracle as po  # only for the erasure-pattern generator (host ints)
+    rows_np = np.zeros((G, k), np.uint8)
+    es = np.zeros(G, np.int64)
+    for g in range(G):
+        es[g], rows_np[g] = po.erasure_pattern(g0 + g, k, m, 0xBE, args.erasures)
+    rows = torch.from_numpy(rows_np).cuda()
+    whole = torch.cat([enc_in, enc_out], dim=1)
+    dec_in = whole[torch.arange(G, device="cuda")[:, None], rows.long()].contiguous()
+    del whole
+    dec_out = torch.empty((G, emax, B), dtype=torch.uint8, device="cuda")
+    dec_rows = torch.empty((G, emax), dtype=torch.uint8, device="cuda")
+    dec_cnt = torch.empty(G, dtype=torch.int32, device="cuda")
+    sh.batch_reserve(k, m, B, G)
+    torch.cuda.synchronize()
+
+    enc_bytes = G * (k + m) * B
+    dec_bytes = int((k + es).sum()) * B
+
+    def step(evs=None):
+        if evs is not None:
+            evs[0].record(stream)
+        rc1 = sh.encode_batch(k, m, B, G, enc_in, enc_out, s)
+        if evs is not None:
+            evs[1].record(stream)
+        rc2 = sh.decode_batch_out(k, m, B, G, dec_in, rows, dec_out, dec_rows, dec_cnt, s)
+        if evs is not None:
+            evs[2].record(stream)
+        assert rc1 == 0 and rc2 == 0
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # correctness guard on the timed buffers: recovered blocks equal the erased originals
+    cnt = dec_cnt.cpu().numpy()
+    assert np.array_equal(cnt, es)
+    g_chk = torch.arange(G, device="cuda")[:, None]
+    ok = torch.equal(dec_out, enc_in[g_chk, dec_rows.long()]) if args.erasures == emax else True
+    assert ok, "decode output mismatch"
+
+    # ---- timed region ----
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        tot = torch.tensor([dec_bytes], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        dec_bytes_all = float(tot.item())
+    else:
+        dec_bytes_all = float(dec_bytes)
+    enc_bytes_all = float(enc_bytes) * world
+    total = (enc_bytes_all + dec_bytes_all) * args.steps
+    value = total / elapsed / 2**30
+    ms_per_step = elapsed / args.steps * 1e3
+
+    if rank == 0:
+        enc_bw = enc_bytes / (enc_ms * 1e-3)
+        dec_bw = dec_bytes / (dec_ms * 1e-3)
+        dom = ("encode", enc_ms, enc_bw, enc_bytes) if enc_ms >= dec_ms else ("decode", dec_ms, dec_bw, dec_bytes)
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        cpu = None if args.no_cpu else cpu_baseline(k, m, B, args.erasures, args.cpu_seconds, threads)
+        line = {
+            "metric": "cauchy_256 encode+decode GiB/s (device-resident), k=200 m=32 ×1400B; %HBM peak",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (PCG32 per block, device-generated; erasure patterns PCG32)",
+            "config": {"workload": f"{G} groups/GPU encode + {G} groups/GPU decode, k={k} m={m} "
+                                   f"B={B} e={args.erasures or 'rand'}",
+                       "k": k, "m": m, "block_bytes": B, "groups_per_gpu": G,
+                       "erasures": args.erasures, "parallelism": f"groups sharded x{world}"},
+            "hbm_frac": round(value * 2**30 / world / HBM_PEAK, 4),
+            "payload_GiBps": round(G * world * k * B * 2 * args.steps / elapsed / 2**30, 3),
+            "ops": {"encode_ms": round(enc_ms, 4), "encode_GBps": round(enc_bw / 1e9, 1),
+                    "decode_ms": round(dec_ms, 4), "decode_GBps": round(dec_bw / 1e9, 1)},
+            "roofline": {"bound": "hbm", "kernel": dom[0], "achieved": round(dom[2] / 1e9, 1),
+                         "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                         "frac": round(dom[2] / HBM_PEAK, 4), "traffic": None,
+                         "alg_bytes_per_launch": dom[3]},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,64 @@
+/*
+ * cauchy_256_batch.h -- batched, device-resident C ABI (new; no counterpart in the reference).
+ *
+ * The reference codes one group per call on one CPU thread (cauchy_256.cpp:1479, :1233). Here a
+ * call codes `groups` independent code groups that already sit in GPU memory (HBM), with the same
+ * per-group semantics and bytes as cauchy_256_encode / cauchy_256_decode. All calls are
+ * asynchronous on `stream` (a hipStream_t, NULL = the library's stream) and enqueue no host
+ * synchronisation, except where noted for invalid parameters.
+ *
+ * Layouts (byte offsets inside one device allocation, no alignment required):
+ *   data      [groups][k][block_bytes]      encode input
+ *   recovery  [groups][m][block_bytes]      encode output
+ *   blocks    [groups][k][block_bytes]      decode blocks (received, in array order)
+ *   rows      [groups][k]                   decode rows (the Block.row fields)
+ *
+ * Return codes: 0 ok, -1 invalid parameters (as the reference), -2 GPU/runtime error.
+ */
+#ifndef SH_AMD_CAUCHY_256_BATCH_H
+#define SH_AMD_CAUCHY_256_BATCH_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Select the device for this process (default 0) and initialise; 0 ok, -2 no GPU. */
+int cauchy_256_batch_init(int device);
+
+/* Encode every group: recovery[g] = cauchy_256_encode(k, m, data[g]). */
+int cauchy_256_encode_batch(int k, int m, int block_bytes, int groups, const void *d_data,
+                            void *d_recovery, void *stream);
+
+/* Decode every group in place, exactly like cauchy_256_decode on (blocks[g], rows[g]). */
+int cauchy_256_decode_batch(int k, int m, int block_bytes, int groups, void *d_blocks,
+                            unsigned char *d_rows, void *stream);
+
+/*
+ * Out-of-place decode: blocks and rows are read only. Group g's recovered originals go to
+ * d_out[g][0 .. e_g-1][block_bytes] (dense, emax = min(k, m) slots per group) in the order the
+ * in-place call would write them (i-th recovery block in array order <- i-th smallest erasure);
+ * d_out_rows[g][i] receives that erasure index and d_out_count[g] = e_g. m >= 2 only.
+ */
+int cauchy_256_decode_batch_out(int k, int m, int block_bytes, int groups, const void *d_blocks,
+                                const unsigned char *d_rows, void *d_out, unsigned char *d_out_rows,
+                                int *d_out_count, void *stream);
+
+/* Pre-allocate the internal decode workspace so later calls allocate nothing (graph capture). */
+int cauchy_256_batch_reserve(int k, int m, int block_bytes, int groups);
+
+/* Synthetic workload: block x of group g0+g = PCG32 Seed((g0+g)*256 + x, cfg) words (the same
+ * stream as the test oracle), written to d_out[groups][n][block_bytes]. */
+int cauchy_256_fill_synthetic(void *d_out, int n, int block_bytes, int groups,
+                              unsigned long long g0, unsigned long long cfg, void *stream);
+
+/* Library's own stream (hipStream_t) and a device synchronize helper for callers without HIP. */
+void *cauchy_256_default_stream(void);
+int cauchy_256_sync(void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SH_AMD_CAUCHY_256_BATCH_H */

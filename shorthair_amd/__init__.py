@@ -1,0 +1,143 @@
+"""shorthair_amd -- MI355X-native Cauchy Reed-Solomon codec (drop-in for catid/shorthair cauchy_256).
+
+The product is the C-ABI shared library ``libcauchy256.so`` (HIP kernels for gfx950 + host code);
+this module is a thin ctypes binding used by the tests and the benchmark. It mirrors the
+reference interface (cauchy_256.h: ``cauchy_256_init`` / ``cauchy_256_encode`` /
+``cauchy_256_decode`` with the same argument meaning and return codes) and exposes the batched
+device-resident API (``include/cauchy_256_batch.h``) on torch tensors.
+
+There is no CPU fallback: if the library is missing this import fails, and without a GPU every
+codec call returns -2 (see the library's stderr message).
+"""
+import ctypes
+import os
+
+__all__ = ["lib", "Block", "CAUCHY_256_VERSION", "cauchy_256_init", "cauchy_256_encode",
+           "cauchy_256_decode", "encode_batch", "decode_batch", "decode_batch_out",
+           "fill_synthetic", "batch_reserve", "default_stream", "sync", "LIB_PATH",
+           "EXPORTED_SYMBOLS"]
+
+CAUCHY_256_VERSION = 2
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcauchy256.so")
+
+# Every symbol declared in include/cauchy_256.h and include/cauchy_256_batch.h.
+EXPORTED_SYMBOLS = [
+    "_cauchy_256_init", "cauchy_256_encode", "cauchy_256_decode",
+    "cauchy_256_batch_init", "cauchy_256_encode_batch", "cauchy_256_decode_batch",
+    "cauchy_256_decode_batch_out", "cauchy_256_batch_reserve", "cauchy_256_fill_synthetic",
+    "cauchy_256_default_stream", "cauchy_256_sync",
+]
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"{LIB_PATH} not built: run `python -m shorthair_amd.build` "
+                      "(the codec has no CPU fallback)")
+
+lib = ctypes.CDLL(LIB_PATH)
+
+
+class Block(ctypes.Structure):
+    """Reference Block descriptor (cauchy_256.h:52-55)."""
+    _fields_ = [("data", ctypes.c_void_p), ("row", ctypes.c_ubyte)]
+
+
+_c = ctypes
+lib._cauchy_256_init.argtypes = [_c.c_int]
+lib._cauchy_256_init.restype = _c.c_int
+lib.cauchy_256_encode.argtypes = [_c.c_int, _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_int]
+lib.cauchy_256_encode.restype = _c.c_int
+lib.cauchy_256_decode.argtypes = [_c.c_int, _c.c_int, _c.c_void_p, _c.c_int]
+lib.cauchy_256_decode.restype = _c.c_int
+lib.cauchy_256_batch_init.argtypes = [_c.c_int]
+lib.cauchy_256_batch_init.restype = _c.c_int
+lib.cauchy_256_encode_batch.argtypes = [_c.c_int] * 4 + [_c.c_void_p] * 3
+lib.cauchy_256_encode_batch.restype = _c.c_int
+lib.cauchy_256_decode_batch.argtypes = [_c.c_int] * 4 + [_c.c_void_p] * 3
+lib.cauchy_256_decode_batch.restype = _c.c_int
+lib.cauchy_256_decode_batch_out.argtypes = [_c.c_int] * 4 + [_c.c_void_p] * 6
+lib.cauchy_256_decode_batch_out.restype = _c.c_int
+lib.cauchy_256_batch_reserve.argtypes = [_c.c_int] * 4
+lib.cauchy_256_batch_reserve.restype = _c.c_int
+lib.cauchy_256_fill_synthetic.argtypes = [_c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
+                                          _c.c_ulonglong, _c.c_ulonglong, _c.c_void_p]
+lib.cauchy_256_fill_synthetic.restype = _c.c_int
+lib.cauchy_256_default_stream.argtypes = []
+lib.cauchy_256_default_stream.restype = _c.c_void_p
+lib.cauchy_256_sync.argtypes = [_c.c_void_p]
+lib.cauchy_256_sync.restype = _c.c_int
+
+
+class CodecError(RuntimeError):
+    pass
+
+
+def _check(rc, what):
+    if rc == -2:
+        raise CodecError(f"{what}: GPU/runtime failure (see stderr)")
+    return rc
+
+
+# ---- reference-shaped single-group API (host buffers; numpy arrays or anything with .ctypes) ----
+
+def cauchy_256_init(version=CAUCHY_256_VERSION):
+    """_cauchy_256_init: 0 ok, -1 version mismatch (reference cauchy_256.cpp:390-399)."""
+    return _check(lib._cauchy_256_init(version), "cauchy_256_init")
+
+
+def cauchy_256_encode(k, m, data_ptrs, recovery_ptr, block_bytes):
+    """data_ptrs: sequence of k integer addresses; recovery_ptr: address of m*block_bytes."""
+    arr = (ctypes.c_void_p * max(k, 1))(*[int(p) for p in data_ptrs])
+    return _check(lib.cauchy_256_encode(k, m, arr, int(recovery_ptr), block_bytes), "encode")
+
+
+def cauchy_256_decode(k, m, blocks, block_bytes):
+    """blocks: ctypes array of Block (modified in place, like the reference)."""
+    return _check(lib.cauchy_256_decode(k, m, blocks, block_bytes), "decode")
+
+
+# ---- batched device-resident API on torch tensors ----
+
+def _ptr(t):
+    return None if t is None else int(t.data_ptr())
+
+
+def _stream(stream):
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    return stream
+
+
+def encode_batch(k, m, block_bytes, groups, data, recovery, stream=None):
+    """data: uint8 cuda tensor [groups][k][B]; recovery: [groups][m][B]."""
+    return _check(lib.cauchy_256_encode_batch(k, m, block_bytes, groups, _ptr(data), _ptr(recovery),
+                                              _stream(stream)), "encode_batch")
+
+
+def decode_batch(k, m, block_bytes, groups, blocks, rows, stream=None):
+    """In place on blocks [groups][k][B] and rows [groups][k] (uint8 cuda tensors)."""
+    return _check(lib.cauchy_256_decode_batch(k, m, block_bytes, groups, _ptr(blocks), _ptr(rows),
+                                              _stream(stream)), "decode_batch")
+
+
+def decode_batch_out(k, m, block_bytes, groups, blocks, rows, out, out_rows, out_count, stream=None):
+    """Read-only blocks/rows; out [groups][min(k,m)][B], out_rows [groups][min(k,m)], out_count int32 [groups]."""
+    return _check(lib.cauchy_256_decode_batch_out(k, m, block_bytes, groups, _ptr(blocks), _ptr(rows),
+                                                  _ptr(out), _ptr(out_rows), _ptr(out_count),
+                                                  _stream(stream)), "decode_batch_out")
+
+
+def fill_synthetic(out, n, block_bytes, groups, g0, cfg, stream=None):
+    return _check(lib.cauchy_256_fill_synthetic(_ptr(out), n, block_bytes, groups, g0, cfg,
+                                                _stream(stream)), "fill_synthetic")
+
+
+def batch_reserve(k, m, block_bytes, groups):
+    return _check(lib.cauchy_256_batch_reserve(k, m, block_bytes, groups), "batch_reserve")
+
+
+def default_stream():
+    return lib.cauchy_256_default_stream()
+
+
+def sync(stream=None):
+    return _check(lib.cauchy_256_sync(stream), "sync")

@@ -1,0 +1,481 @@
+// Host side of libcauchy256.so: the drop-in cauchy_256.h ABI and the batched device ABI.
+//
+// Every coding call runs on the GPU. The single-group reference entry points
+// (cauchy_256_encode / cauchy_256_decode, reference cauchy_256.cpp:1479 / :1233) gather the
+// caller's host blocks into pinned staging, run the batched kernels with groups = 1 and scatter
+// the result back; there is deliberately no CPU implementation of the codec in this library.
+// Without a usable GPU every call prints an error and returns -2.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <utility>
+#include <vector>
+
+#include "../../include/cauchy_256.h"
+#include "../../include/cauchy_256_batch.h"
+#include "cauchy_math.hpp"
+#include "kernels.hpp"
+
+namespace {
+
+using sh::Geometry;
+
+#define SH_CHECK(expr)                                                                        \
+    do {                                                                                      \
+        hipError_t _e = (expr);                                                               \
+        if (_e != hipSuccess) {                                                               \
+            std::fprintf(stderr, "libcauchy256: %s failed: %s (%s:%d)\n", #expr,             \
+                         hipGetErrorString(_e), __FILE__, __LINE__);                          \
+            return -2;                                                                        \
+        }                                                                                     \
+    } while (0)
+
+inline int round4(int x) { return (x + 3) & ~3; }
+
+// Grow-only device buffer.
+struct DevBuf {
+    void *p = nullptr;
+    size_t n = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= n) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        if (hipMalloc(&p, bytes) != hipSuccess) {
+            std::fprintf(stderr, "libcauchy256: hipMalloc(%zu) failed\n", bytes);
+            return -2;
+        }
+        n = bytes;
+        return 0;
+    }
+};
+
+struct PinnedBuf {
+    void *p = nullptr;
+    size_t n = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= n) return 0;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+            std::fprintf(stderr, "libcauchy256: hipHostMalloc(%zu) failed\n", bytes);
+            return -2;
+        }
+        n = bytes;
+        return 0;
+    }
+};
+
+struct Context {
+    std::mutex mu;          // guards lazy state (tables, caches, workspace, staging)
+    bool ready = false;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint64_t *d_rowbytes = nullptr;   // 256 x 8 bytes
+    uint8_t *d_exp = nullptr;         // 512
+    uint16_t *d_log = nullptr;        // 256
+    // (k, m) -> device generator: [m][round4(k)] coefficients (row 0 = ones) for encode,
+    // followed by the raw (m-1) x k rows 1..m-1 for decode setup.
+    std::map<std::pair<int, int>, uint8_t *> gens;
+    DevBuf ws;                        // decode workspace
+    // single-group staging, guarded by stage_mu for the whole call
+    std::mutex stage_mu;
+    PinnedBuf h_stage;
+    DevBuf d_stage;
+};
+
+Context &ctx() {
+    static Context c;
+    return c;
+}
+
+int init_locked(Context &c, int device) {
+    if (c.ready) return 0;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        std::fprintf(stderr, "libcauchy256: no HIP device available; the codec runs only on the GPU\n");
+        return -2;
+    }
+    if (device < 0 || device >= n) device = 0;
+    SH_CHECK(hipSetDevice(device));
+    SH_CHECK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    const sh::GF256 &f = sh::gf();
+    uint64_t rb[256];
+    for (int v = 0; v < 256; ++v) {
+        uint64_t w = 0;
+        for (int b = 0; b < 8; ++b) w |= static_cast<uint64_t>(f.row_bytes[v][b]) << (8 * b);
+        rb[v] = w;
+    }
+    SH_CHECK(hipMalloc(&c.d_rowbytes, sizeof rb));
+    SH_CHECK(hipMemcpy(c.d_rowbytes, rb, sizeof rb, hipMemcpyHostToDevice));
+    SH_CHECK(hipMalloc(&c.d_exp, 512));
+    SH_CHECK(hipMemcpy(c.d_exp, f.exp, 512, hipMemcpyHostToDevice));
+    SH_CHECK(hipMalloc(&c.d_log, 512));
+    SH_CHECK(hipMemcpy(c.d_log, f.log, 512, hipMemcpyHostToDevice));
+    c.device = device;
+    c.ready = true;
+    return 0;
+}
+
+int ensure_init(Context &c) {
+    std::lock_guard<std::mutex> g(c.mu);
+    return init_locked(c, c.device);
+}
+
+// Device generator for (k, m), m >= 2, k + m <= 256. Cached; created once per shape.
+uint8_t *generator(Context &c, int k, int m) {
+    std::lock_guard<std::mutex> g(c.mu);
+    auto it = c.gens.find({k, m});
+    if (it != c.gens.end()) return it->second;
+    const std::vector<uint8_t> G = sh::generator_matrix(k, m);
+    const int ld = round4(k);
+    std::vector<uint8_t> host(static_cast<size_t>(m) * ld + static_cast<size_t>(m - 1) * k, 0);
+    for (int y = 0; y < m; ++y) std::memcpy(&host[static_cast<size_t>(y) * ld], &G[static_cast<size_t>(y) * k], k);
+    std::memcpy(&host[static_cast<size_t>(m) * ld], &G[k], static_cast<size_t>(m - 1) * k);
+    uint8_t *d = nullptr;
+    if (hipMalloc(&d, host.size()) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, host.data(), host.size(), hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    c.gens[{k, m}] = d;
+    return d;
+}
+
+hipStream_t pick(void *stream) {
+    return stream ? static_cast<hipStream_t>(stream) : ctx().stream;
+}
+
+// ---- batched encode ----
+int encode_batch(int k, int m, int B, int groups, const uint8_t *d_in, uint8_t *d_out,
+                 hipStream_t s) {
+    Context &c = ctx();
+    if (int rc = ensure_init(c)) return rc;
+    if (groups <= 0 || m <= 0 || k <= 0 || B <= 0) return 0;
+    const long long in_gs = static_cast<long long>(k) * B, out_gs = static_cast<long long>(m) * B;
+    if (k <= 1) {  // reference cauchy_256.cpp:1485-1493
+        SH_CHECK(sh::launch_copy_first(d_in, in_gs, d_out, out_gs, m, B, groups, s));
+        return 0;
+    }
+    const bool valid = (k + m <= 256) && (B % 8 == 0);
+    if (m == 1 || !valid) {
+        // Row 0 (plain XOR, any B) is written even when the parameters are then rejected
+        // (reference cauchy_256.cpp:1496-1511).
+        SH_CHECK(sh::launch_xor_rows(d_in, in_gs, k, d_out, out_gs, B, groups, s));
+        return valid ? 0 : -1;
+    }
+    uint8_t *gen = generator(c, k, m);
+    if (!gen) return -2;
+    sh::ApplyArgs a{};
+    a.in = d_in;
+    a.in_gstride = in_gs;
+    a.in_bstride = B;
+    a.n_in = k;
+    a.out = d_out;
+    a.out_gstride = out_gs;
+    a.out_bstride = B;
+    a.n_out = m;  // row 0 = coefficient 1 everywhere: M(1) is the identity, i.e. plain XOR
+    a.n_out_g = nullptr;
+    a.coef = gen;
+    a.coef_gstride = 0;
+    a.coef_ld = round4(k);
+    a.rowbytes = c.d_rowbytes;
+    a.groups = groups;
+    a.geo = sh::make_geometry(B);
+    SH_CHECK(sh::launch_apply(a, false, s));
+    return 0;
+}
+
+// Workspace carve for decode of `groups` groups.
+struct DecodeWS {
+    int emax, ldA, ldB;
+    int *e;
+    uint8_t *rec_idx, *erasures, *coefA, *coefB, *residual, *recovered;
+    long long coefA_gs, coefB_gs;
+};
+
+size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool need_recovered) {
+    w.emax = std::min(k, m);
+    w.ldA = round4(k);
+    w.ldB = round4(w.emax);
+    w.coefA_gs = static_cast<long long>(w.emax) * w.ldA;
+    w.coefB_gs = static_cast<long long>(w.emax) * w.ldB;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        uint8_t *p = base ? base + off : nullptr;
+        off += (bytes + 255) & ~static_cast<size_t>(255);
+        return p;
+    };
+    const size_t G = static_cast<size_t>(groups);
+    w.e = reinterpret_cast<int *>(take(G * sizeof(int)));
+    w.rec_idx = take(G * w.emax);
+    w.erasures = take(G * w.emax);
+    w.coefA = take(G * w.coefA_gs);
+    w.coefB = take(G * w.coefB_gs);
+    w.residual = take(G * w.emax * static_cast<size_t>(B));
+    w.recovered = need_recovered ? take(G * w.emax * static_cast<size_t>(B)) : nullptr;
+    return off;
+}
+
+// Common decode core (m >= 2, valid params): writes recovered blocks densely into `dst`
+// ([G][emax][B]) and leaves per-group e / rec_idx / erasures in the workspace.
+int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_blocks,
+                const uint8_t *d_rows, DecodeWS &w, uint8_t *dst, hipStream_t s) {
+    uint8_t *gen = generator(c, k, m);
+    if (!gen) return -2;
+    sh::DecodeSetupArgs sa{};
+    sa.k = k;
+    sa.m = m;
+    sa.rows = d_rows;
+    sa.rows_gstride = k;
+    sa.gen = gen + static_cast<size_t>(m) * round4(k);
+    sa.gf_exp = c.d_exp;
+    sa.gf_log = c.d_log;
+    sa.emax = w.emax;
+    sa.e_out = w.e;
+    sa.rec_idx = w.rec_idx;
+    sa.erasures = w.erasures;
+    sa.coefA = w.coefA;
+    sa.coefA_gstride = w.coefA_gs;
+    sa.ldA = w.ldA;
+    sa.coefB = w.coefB;
+    sa.coefB_gstride = w.coefB_gs;
+    sa.ldB = w.ldB;
+    SH_CHECK(sh::launch_decode_setup(sa, groups, s));
+
+    const Geometry geo = sh::make_geometry(B);
+    // Stage A: residual_i = R_i + sum_{orig j} M(C[r_i][row_j]) d_j  (per-group coefficients)
+    sh::ApplyArgs a{};
+    a.in = d_blocks;
+    a.in_gstride = static_cast<long long>(k) * B;
+    a.in_bstride = B;
+    a.n_in = k;
+    a.out = w.residual;
+    a.out_gstride = static_cast<long long>(w.emax) * B;
+    a.out_bstride = B;
+    a.n_out = w.emax;
+    a.n_out_g = w.e;
+    a.coef = w.coefA;
+    a.coef_gstride = w.coefA_gs;
+    a.coef_ld = w.ldA;
+    a.rowbytes = c.d_rowbytes;
+    a.groups = groups;
+    a.geo = geo;
+    SH_CHECK(sh::launch_apply(a, true, s));
+    // Stage B: recovered_l = sum_i M(S^-1[l][i]) residual_i
+    sh::ApplyArgs b = a;
+    b.in = w.residual;
+    b.in_gstride = static_cast<long long>(w.emax) * B;
+    b.n_in = w.emax;
+    b.out = dst;
+    b.coef = w.coefB;
+    b.coef_gstride = w.coefB_gs;
+    b.coef_ld = w.ldB;
+    SH_CHECK(sh::launch_apply(b, true, s));
+    return 0;
+}
+
+// Invalid parameters: the reference returns -1 only when a group actually has something to
+// recover (cauchy_256.cpp:1266-1273); find out on the host (rare path, synchronous).
+int invalid_decode_status(int k, int groups, const uint8_t *d_rows, hipStream_t s) {
+    std::vector<uint8_t> rows(static_cast<size_t>(groups) * k);
+    SH_CHECK(hipMemcpyAsync(rows.data(), d_rows, rows.size(), hipMemcpyDeviceToHost, s));
+    SH_CHECK(hipStreamSynchronize(s));
+    for (uint8_t r : rows)
+        if (r >= k) return -1;
+    return 0;
+}
+
+int decode_batch(int k, int m, int B, int groups, uint8_t *d_blocks, uint8_t *d_rows,
+                 hipStream_t s) {
+    Context &c = ctx();
+    if (int rc = ensure_init(c)) return rc;
+    if (groups <= 0 || k <= 0) return 0;
+    if (k <= 1) {  // cauchy_256.cpp:1236-1240
+        SH_CHECK(sh::launch_decode_k1(d_rows, k, groups, s));
+        return 0;
+    }
+    if (m == 1) {  // cauchy_256.cpp:1243-1246 (no parameter check on this path)
+        SH_CHECK(sh::launch_decode_m1(d_blocks, static_cast<long long>(k) * B, d_rows, k, k, B, groups, s));
+        return 0;
+    }
+    if (k + m > 256 || B % 8 != 0) return invalid_decode_status(k, groups, d_rows, s);
+    DecodeWS w{};
+    const size_t need = carve(w, nullptr, k, m, B, groups, true);
+    {
+        std::lock_guard<std::mutex> g(c.mu);
+        if (int rc = c.ws.ensure(need)) return rc;
+        carve(w, static_cast<uint8_t *>(c.ws.p), k, m, B, groups, true);
+    }
+    if (int rc = decode_core(c, k, m, B, groups, d_blocks, d_rows, w, w.recovered, s)) return rc;
+    sh::ScatterArgs sc{};
+    sc.src = w.recovered;
+    sc.src_gstride = static_cast<long long>(w.emax) * B;
+    sc.blocks = d_blocks;
+    sc.blocks_gstride = static_cast<long long>(k) * B;
+    sc.rows = d_rows;
+    sc.rows_gstride = k;
+    sc.e = w.e;
+    sc.rec_idx = w.rec_idx;
+    sc.erasures = w.erasures;
+    sc.emax = w.emax;
+    sc.B = B;
+    SH_CHECK(sh::launch_scatter(sc, groups, s));
+    return 0;
+}
+
+}  // namespace
+
+// =============================================================================================
+// Batched device ABI (cauchy_256_batch.h)
+// =============================================================================================
+extern "C" int cauchy_256_batch_init(int device) {
+    Context &c = ctx();
+    std::lock_guard<std::mutex> g(c.mu);
+    return init_locked(c, device);
+}
+
+extern "C" int cauchy_256_encode_batch(int k, int m, int block_bytes, int groups,
+                                       const void *d_data, void *d_recovery, void *stream) {
+    return encode_batch(k, m, block_bytes, groups, static_cast<const uint8_t *>(d_data),
+                        static_cast<uint8_t *>(d_recovery), pick(stream));
+}
+
+extern "C" int cauchy_256_decode_batch(int k, int m, int block_bytes, int groups, void *d_blocks,
+                                       unsigned char *d_rows, void *stream) {
+    return decode_batch(k, m, block_bytes, groups, static_cast<uint8_t *>(d_blocks), d_rows,
+                        pick(stream));
+}
+
+extern "C" int cauchy_256_decode_batch_out(int k, int m, int block_bytes, int groups,
+                                           const void *d_blocks, const unsigned char *d_rows,
+                                           void *d_out, unsigned char *d_out_rows,
+                                           int *d_out_count, void *stream) {
+    Context &c = ctx();
+    if (int rc = ensure_init(c)) return rc;
+    if (groups <= 0) return 0;
+    if (k < 2 || m < 2) return -1;
+    hipStream_t s = pick(stream);
+    if (k + m > 256 || block_bytes % 8 != 0) return invalid_decode_status(k, groups, d_rows, s);
+    DecodeWS w{};
+    const size_t need = carve(w, nullptr, k, m, block_bytes, groups, false);
+    {
+        std::lock_guard<std::mutex> g(c.mu);
+        if (int rc = c.ws.ensure(need)) return rc;
+        carve(w, static_cast<uint8_t *>(c.ws.p), k, m, block_bytes, groups, false);
+    }
+    if (int rc = decode_core(c, k, m, block_bytes, groups, static_cast<const uint8_t *>(d_blocks),
+                             d_rows, w, static_cast<uint8_t *>(d_out), s))
+        return rc;
+    SH_CHECK(hipMemcpyAsync(d_out_rows, w.erasures, static_cast<size_t>(groups) * w.emax,
+                            hipMemcpyDeviceToDevice, s));
+    SH_CHECK(hipMemcpyAsync(d_out_count, w.e, static_cast<size_t>(groups) * sizeof(int),
+                            hipMemcpyDeviceToDevice, s));
+    return 0;
+}
+
+extern "C" int cauchy_256_batch_reserve(int k, int m, int block_bytes, int groups) {
+    Context &c = ctx();
+    if (int rc = ensure_init(c)) return rc;
+    if (k < 2 || m < 2 || k + m > 256) return 0;
+    DecodeWS w{};
+    const size_t need = carve(w, nullptr, k, m, block_bytes, groups, true);
+    if (!generator(c, k, m)) return -2;
+    std::lock_guard<std::mutex> g(c.mu);
+    return c.ws.ensure(need);
+}
+
+extern "C" int cauchy_256_fill_synthetic(void *d_out, int n, int block_bytes, int groups,
+                                         unsigned long long g0, unsigned long long cfg,
+                                         void *stream) {
+    Context &c = ctx();
+    if (int rc = ensure_init(c)) return rc;
+    SH_CHECK(sh::launch_fill(static_cast<uint8_t *>(d_out), static_cast<long long>(n) * block_bytes,
+                             n, block_bytes, groups, g0, cfg, pick(stream)));
+    return 0;
+}
+
+extern "C" void *cauchy_256_default_stream(void) {
+    Context &c = ctx();
+    if (ensure_init(c)) return nullptr;
+    return c.stream;
+}
+
+extern "C" int cauchy_256_sync(void *stream) {
+    Context &c = ctx();
+    if (int rc = ensure_init(c)) return rc;
+    SH_CHECK(hipStreamSynchronize(pick(stream)));
+    return 0;
+}
+
+// =============================================================================================
+// Drop-in single-group ABI (cauchy_256.h). One group per call through pinned staging.
+// =============================================================================================
+extern "C" int _cauchy_256_init(int expected_version) {
+    if (expected_version != CAUCHY_256_VERSION) return -1;  // reference cauchy_256.cpp:392-394
+    Context &c = ctx();
+    std::lock_guard<std::mutex> g(c.mu);
+    return init_locked(c, c.device);
+}
+
+extern "C" int cauchy_256_encode(int k, int m, const unsigned char *data_ptrs[],
+                                 void *recovery_blocks, int block_bytes) {
+    Context &c = ctx();
+    if (int rc = ensure_init(c)) return rc;
+    if (k <= 0 || m <= 0 || block_bytes <= 0) return 0;
+    const int kin = k <= 1 ? 1 : k;
+    const size_t in_bytes = static_cast<size_t>(kin) * block_bytes;
+    const size_t out_bytes = static_cast<size_t>(m) * block_bytes;
+    std::lock_guard<std::mutex> g(c.stage_mu);  // one staging area; calls serialise like Shorthair's
+    if (int rc = c.h_stage.ensure(in_bytes + out_bytes)) return rc;
+    if (int rc = c.d_stage.ensure(in_bytes + out_bytes)) return rc;
+    uint8_t *h = static_cast<uint8_t *>(c.h_stage.p);
+    uint8_t *d = static_cast<uint8_t *>(c.d_stage.p);
+    for (int x = 0; x < kin; ++x) std::memcpy(h + static_cast<size_t>(x) * block_bytes, data_ptrs[x], block_bytes);
+    SH_CHECK(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, c.stream));
+    const int rc = encode_batch(k, m, block_bytes, 1, d, d + in_bytes, c.stream);
+    if (rc == -2) return rc;
+    // Like the reference, a rejected call has still written recovery row 0.
+    const size_t copy = (rc == 0) ? out_bytes : static_cast<size_t>(block_bytes);
+    SH_CHECK(hipMemcpyAsync(h + in_bytes, d + in_bytes, copy, hipMemcpyDeviceToHost, c.stream));
+    SH_CHECK(hipStreamSynchronize(c.stream));
+    std::memcpy(recovery_blocks, h + in_bytes, copy);
+    return rc;
+}
+
+extern "C" int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes) {
+    Context &c = ctx();
+    if (int rc = ensure_init(c)) return rc;
+    if (k <= 1) {  // cauchy_256.cpp:1236-1240: no data touched
+        if (k == 1) blocks[0].row = 0;
+        return 0;
+    }
+    if (block_bytes <= 0) return 0;
+    const size_t data_bytes = static_cast<size_t>(k) * block_bytes;
+    std::lock_guard<std::mutex> g(c.stage_mu);
+    if (int rc = c.h_stage.ensure(data_bytes + 256)) return rc;
+    if (int rc = c.d_stage.ensure(data_bytes + 256)) return rc;
+    uint8_t *h = static_cast<uint8_t *>(c.h_stage.p);
+    uint8_t *d = static_cast<uint8_t *>(c.d_stage.p);
+    for (int i = 0; i < k; ++i) {
+        std::memcpy(h + static_cast<size_t>(i) * block_bytes, blocks[i].data, block_bytes);
+        h[data_bytes + i] = blocks[i].row;
+    }
+    SH_CHECK(hipMemcpyAsync(d, h, data_bytes + k, hipMemcpyHostToDevice, c.stream));
+    const int rc = decode_batch(k, m, block_bytes, 1, d, d + data_bytes, c.stream);
+    if (rc != 0) return rc;
+    SH_CHECK(hipMemcpyAsync(h, d, data_bytes + k, hipMemcpyDeviceToHost, c.stream));
+    SH_CHECK(hipStreamSynchronize(c.stream));
+    // Write back only what the codec may change: the blocks whose row was >= k (they receive
+    // recovered data) -- originals are never modified (reference row contract).
+    for (int i = 0; i < k; ++i) {
+        if (blocks[i].row >= k) {
+            std::memcpy(blocks[i].data, h + static_cast<size_t>(i) * block_bytes, block_bytes);
+            blocks[i].row = h[data_bytes + i];
+        }
+    }
+    return 0;
+}

@@ -1,0 +1,522 @@
+// HIP kernels (gfx950 / CDNA4) for the batched Cauchy Reed-Solomon codec.
+//
+// Data model (bitmatrix CRS, reference catid/shorthair cauchy_256.cpp:1398-1578): a block of B bytes
+// is 8 sub-blocks of sub = B/8 bytes. Generator element c acts as the 8x8 GF(2) matrix M(c) whose
+// row b is the byte c*2^b in GF(256)/0x187: output sub-block b ^= input sub-block a for every bit
+// a set in c*2^b. Every byte position p in [0, sub) -- and every bit of it -- is an independent
+// "column", so a lane owns one 32-bit word of columns (bytes 4q..4q+3 of each sub-block) and runs
+// the whole group's bitmatrix on it with word-wide XORs. M is a ring homomorphism
+// (M(a)M(b) = M(ab)), which is what lets decode use a GF(256) inverse.
+//
+// Layout in HBM: a batch is `groups` code groups stored back to back; inside a group, blocks are
+// contiguous B-byte rows ([G][n][B]). Sub-block starts are generally not 4-byte aligned
+// (B = 1400 -> sub = 175); gfx950 global loads/stores accept unaligned dword addresses, so a lane
+// reads its word directly. The last word of a sub-block holds `tail` = sub - 4*(nq-1) valid bytes:
+// it is loaded right-aligned (never reading past the sub-block) and stored byte-exact.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.hpp"
+
+namespace sh {
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // a ^ b ^ c in one VALU op
+}
+
+__device__ __forceinline__ uint32_t ld32(const uint8_t *p) {
+    uint32_t w;
+    __builtin_memcpy(&w, p, 4);  // unaligned global_load_dword
+    return w;
+}
+
+__device__ __forceinline__ void st32(uint8_t *p, uint32_t w) { __builtin_memcpy(p, &w, 4); }
+
+// Column geometry of one lane: byte offset of its word inside a sub-block, how far the load is
+// shifted back to stay inside the sub-block, and how many bytes it may store.
+struct LaneCol {
+    int off;    // byte offset of the (possibly shifted) load inside the sub-block
+    int shr;    // right shift (bits) applied after the load
+    int nbytes; // valid bytes (1..4)
+};
+
+__device__ __forceinline__ LaneCol lane_col(int q, const Geometry &geo) {
+    LaneCol c;
+    const bool last = (q == geo.nq - 1);
+    const int valid = last ? geo.tail : 4;
+    // A short last word is loaded from (4q - (4 - valid)) so the load ends at the sub-block end.
+    // Only possible when sub >= 4; tiny sub-blocks (B < 32) take the byte path instead.
+    const int back = (geo.sub >= 4) ? (4 - valid) : 0;
+    c.off = 4 * q - back;
+    c.shr = 8 * back;
+    c.nbytes = valid;
+    return c;
+}
+
+__device__ __forceinline__ uint32_t load_col(const uint8_t *sb, const LaneCol &c, bool bytewise) {
+    if (!bytewise) return ld32(sb + c.off) >> c.shr;
+    uint32_t w = 0;
+    for (int i = 0; i < c.nbytes; ++i) w |= static_cast<uint32_t>(sb[c.off + i]) << (8 * i);
+    return w;
+}
+
+__device__ __forceinline__ void store_col(uint8_t *sb, int q, const LaneCol &c, uint32_t w) {
+    uint8_t *p = sb + 4 * q;
+    if (c.nbytes == 4) {
+        st32(p, w);
+    } else {
+        for (int i = 0; i < c.nbytes; ++i) p[i] = static_cast<uint8_t>(w >> (8 * i));
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Generic bitmatrix apply with RUNTIME coefficients:
+//     out[g][o] = sum_j M(coef[g][o][j]) * in[g][j]        (o in [0, n_out_g), j in [0, n_in))
+// Per input j a lane builds the two 4-bit window tables of its 8 sub-block words (reference
+// win_encode, cauchy_256.cpp:1426-1445, 22 XORs) and then folds, for each output sub-block b,
+// lo-table[nibble] ^ hi-table[nibble] into the accumulator with one 3-input XOR. The coefficient is
+// wave-uniform, so the table index is an SGPR (hipcc lowers it to s_set_gpr_idx moves).
+// R output rows per launch row-chunk (grid.y). PER_GROUP: coefficients differ per group and the
+// wave must hold a single group (grid.z = group); otherwise lanes are flattened over (g, q).
+// ---------------------------------------------------------------------------------------------
+template <int R, bool PER_GROUP>
+__global__ __launch_bounds__(256) void apply_generic(ApplyArgs a) {
+    int g, q;
+    if (PER_GROUP) {
+        g = blockIdx.z;
+        q = blockIdx.x * blockDim.x + threadIdx.x;
+        if (q >= a.geo.nq) return;
+    } else {
+        const long long t = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+        g = static_cast<int>(t / a.geo.nq);
+        q = static_cast<int>(t - static_cast<long long>(g) * a.geo.nq);
+        if (g >= a.groups) return;
+    }
+    const int n_out = PER_GROUP && a.n_out_g ? a.n_out_g[g] : a.n_out;
+    const int o0 = blockIdx.y * R;
+    if (o0 >= n_out) return;
+    const int nrows = min(R, n_out - o0);
+
+    const Geometry geo = a.geo;
+    const LaneCol col = lane_col(q, geo);
+    const bool bytewise = geo.sub < 4;
+    const uint8_t *in_g = a.in + static_cast<long long>(g) * a.in_gstride;
+    const uint8_t *coef = a.coef + (PER_GROUP ? static_cast<long long>(g) * a.coef_gstride : 0) +
+                          static_cast<long long>(o0) * a.coef_ld;
+
+    uint32_t acc[R][8];
+#pragma unroll
+    for (int o = 0; o < R; ++o)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[o][b] = 0;
+
+    for (int j4 = 0; j4 < a.n_in; j4 += 4) {
+        uint32_t cw[R];
+#pragma unroll
+        for (int o = 0; o < R; ++o)
+            cw[o] = (o < nrows) ? *reinterpret_cast<const uint32_t *>(coef + o * a.coef_ld + j4) : 0u;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int j = j4 + jj;
+            if (j >= a.n_in) break;
+            uint32_t any = 0;
+#pragma unroll
+            for (int o = 0; o < R; ++o) any |= (cw[o] >> (8 * jj)) & 0xffu;
+            if (!any) continue;
+            const uint8_t *blk = in_g + static_cast<long long>(j) * a.in_bstride;
+            uint32_t t0[16], t1[16];
+            t0[0] = 0;
+            t1[0] = 0;
+            t0[1] = load_col(blk + 0 * geo.sub, col, bytewise);
+            t0[2] = load_col(blk + 1 * geo.sub, col, bytewise);
+            t0[4] = load_col(blk + 2 * geo.sub, col, bytewise);
+            t0[8] = load_col(blk + 3 * geo.sub, col, bytewise);
+            t1[1] = load_col(blk + 4 * geo.sub, col, bytewise);
+            t1[2] = load_col(blk + 5 * geo.sub, col, bytewise);
+            t1[4] = load_col(blk + 6 * geo.sub, col, bytewise);
+            t1[8] = load_col(blk + 7 * geo.sub, col, bytewise);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                uint32_t *t = h ? t1 : t0;
+                t[3] = t[1] ^ t[2];
+                t[5] = t[1] ^ t[4];
+                t[6] = t[2] ^ t[4];
+                t[7] = t[3] ^ t[4];
+                t[9] = t[1] ^ t[8];
+                t[10] = t[2] ^ t[8];
+                t[11] = t[3] ^ t[8];
+                t[12] = t[4] ^ t[8];
+                t[13] = t[5] ^ t[8];
+                t[14] = t[6] ^ t[8];
+                t[15] = t[7] ^ t[8];
+            }
+#pragma unroll
+            for (int o = 0; o < R; ++o) {
+                const uint32_t c = (cw[o] >> (8 * jj)) & 0xffu;
+                if (c == 0) continue;
+                const uint64_t rb = a.rowbytes[c];
+#pragma unroll
+                for (int b = 0; b < 8; ++b) {
+                    const uint32_t s = static_cast<uint32_t>(rb >> (8 * b)) & 0xffu;
+                    acc[o][b] = xor3(acc[o][b], t0[s & 15], t1[s >> 4]);
+                }
+            }
+        }
+    }
+
+    uint8_t *out_g = a.out + static_cast<long long>(g) * a.out_gstride;
+#pragma unroll
+    for (int o = 0; o < R; ++o) {
+        if (o >= nrows) break;
+        uint8_t *blk = out_g + static_cast<long long>(o0 + o) * a.out_bstride;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) store_col(blk + b * geo.sub, q, col, acc[o][b]);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Plain XOR of n_in blocks (any byte count): the parity row 0 (reference cauchy_256.cpp:1496-1500,
+// written before parameter validation) and m == 1 encode. One thread per 4-byte word.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void xor_rows(const uint8_t *in, long long in_gstride, int n_in,
+                                                uint8_t *out, long long out_gstride, int B,
+                                                int groups) {
+    const int nw = (B + 3) / 4;
+    const long long t = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int g = static_cast<int>(t / nw);
+    const int w = static_cast<int>(t - static_cast<long long>(g) * nw);
+    if (g >= groups) return;
+    const int nb = min(4, B - 4 * w);
+    const uint8_t *src = in + g * in_gstride + 4 * w;
+    uint8_t *dst = out + g * out_gstride + 4 * w;
+    if (nb == 4) {
+        uint32_t x = 0;
+        for (int j = 0; j < n_in; ++j) x ^= ld32(src + static_cast<long long>(j) * B);
+        st32(dst, x);
+    } else {
+        for (int i = 0; i < nb; ++i) {
+            uint8_t x = 0;
+            for (int j = 0; j < n_in; ++j) x ^= src[static_cast<long long>(j) * B + i];
+            dst[i] = x;
+        }
+    }
+}
+
+// k <= 1 encode: every output row is a copy of data block 0 (cauchy_256.cpp:1485-1493).
+__global__ __launch_bounds__(256) void copy_first(const uint8_t *in, long long in_gstride,
+                                                  uint8_t *out, long long out_gstride, int m,
+                                                  int B, int groups) {
+    const long long t = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const long long per = static_cast<long long>(m) * B;
+    const int g = static_cast<int>(t / per);
+    if (g >= groups) return;
+    const long long r = t - static_cast<long long>(g) * per;
+    const int p = static_cast<int>(r % B);
+    out[g * out_gstride + r] = in[g * in_gstride + p];
+}
+
+// ---------------------------------------------------------------------------------------------
+// Decode setup, one 64-lane workgroup per group (reference sort_blocks + generate_bitmatrix,
+// cauchy_256.cpp:522-554, :691-774, restated in GF(256)):
+//   * originals (row < k) / recovery blocks (row >= k) in array order; erasures = missing
+//     original rows ascending; e = number of recovery blocks (0 -> nothing to do);
+//   * stage-A coefficients  A[i][j]: residual_i = R_i + sum_{orig j} C[r_i][row_j] * d_j
+//     (= 1 on block rec[i] itself, 0 on the other recovery blocks);
+//   * stage-B coefficients  S^-1 with S[i][l] = C[r_i][erasure_l], by Gauss-Jordan in LDS.
+// The recovered erasure l is then sum_i M(S^-1[l][i]) residual_i; it goes to the l-th recovery
+// block in array order, whose row becomes erasure_l (reference row contract, :548-553, :770).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
+    const int g = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int k = a.k;
+    __shared__ uint8_t s_exp[512];
+    __shared__ uint8_t s_log[256];
+    __shared__ uint8_t s_rows[256];
+    __shared__ uint8_t s_present[256];
+    __shared__ uint8_t s_rec[256];      // array index of the i-th recovery block
+    __shared__ uint8_t s_rrow[256];     // its generator row r_i = row - k
+    __shared__ uint8_t s_era[256];      // i-th erased original row
+    __shared__ uint8_t s_mat[128 * 256];  // [S | I] rows of width 2e (e <= 128)
+    __shared__ int s_piv;
+
+    for (int i = lane; i < 512; i += 64) s_exp[i] = a.gf_exp[i];
+    for (int i = lane; i < 256; i += 64) {
+        s_log[i] = static_cast<uint8_t>(a.gf_log[i]);
+        s_present[i] = 0;
+    }
+    const uint8_t *rows = a.rows + static_cast<long long>(g) * a.rows_gstride;
+    for (int j = lane; j < k; j += 64) s_rows[j] = rows[j];
+    __syncthreads();
+    for (int j = lane; j < k; j += 64)
+        if (s_rows[j] < k) s_present[s_rows[j]] = 1;
+    __syncthreads();
+
+    // Ordered compaction with wave ballots (64 lanes = one wave).
+    int nrec = 0;
+    for (int base = 0; base < k; base += 64) {
+        const int j = base + lane;
+        const bool isrec = (j < k) && (s_rows[j] >= k);
+        const unsigned long long mask = __ballot(isrec);
+        if (isrec) {
+            const int pos = nrec + __popcll(mask & ((1ull << lane) - 1ull));
+            s_rec[pos] = static_cast<uint8_t>(j);
+            s_rrow[pos] = static_cast<uint8_t>(s_rows[j] - k);
+        }
+        nrec += __popcll(mask);
+    }
+    int nera = 0;
+    for (int base = 0; base < k; base += 64) {
+        const int x = base + lane;
+        const bool miss = (x < k) && !s_present[x];
+        const unsigned long long mask = __ballot(miss);
+        if (miss) {
+            const int pos = nera + __popcll(mask & ((1ull << lane) - 1ull));
+            if (pos < 256) s_era[pos] = static_cast<uint8_t>(x);
+        }
+        nera += __popcll(mask);
+    }
+    __syncthreads();
+    const int e = nrec;
+    if (lane == 0) a.e_out[g] = e;
+    if (e == 0) return;
+    // (A caller that hands more recovery blocks than erasures breaks the reference's
+    //  precondition; we clamp like the reference's erasure scan, cauchy_256.cpp:548.)
+    const int emax = a.emax;
+
+    uint8_t *rec_idx = a.rec_idx + static_cast<long long>(g) * emax;
+    uint8_t *era = a.erasures + static_cast<long long>(g) * emax;
+    for (int i = lane; i < e; i += 64) {
+        rec_idx[i] = s_rec[i];
+        era[i] = (i < nera) ? s_era[i] : 0;
+    }
+
+    auto gmul = [&](uint32_t x, uint32_t y) -> uint32_t {
+        return (x && y) ? s_exp[s_log[x] + s_log[y]] : 0u;
+    };
+    auto C = [&](int r, int x) -> uint32_t {
+        return r == 0 ? 1u : a.gen[static_cast<long long>(r - 1) * k + x];
+    };
+
+    // Stage-A coefficients, row-major [i][j], leading dimension ldA.
+    uint8_t *A = a.coefA + static_cast<long long>(g) * a.coefA_gstride;
+    for (int i = 0; i < e; ++i) {
+        const int r = s_rrow[i];
+        for (int j = lane; j < a.ldA; j += 64) {
+            uint32_t c = 0;
+            if (j < k) {
+                const int row = s_rows[j];
+                c = row < k ? C(r, row) : (j == s_rec[i] ? 1u : 0u);
+            }
+            A[static_cast<long long>(i) * a.ldA + j] = static_cast<uint8_t>(c);
+        }
+    }
+
+    // Gauss-Jordan on [S | I] over GF(256).
+    const int w = 2 * e;
+    for (int i = 0; i < e; ++i)
+        for (int c = lane; c < w; c += 64)
+            s_mat[i * w + c] = static_cast<uint8_t>(c < e ? C(s_rrow[i], s_era[c]) : (c - e == i ? 1 : 0));
+    __syncthreads();
+    for (int col = 0; col < e; ++col) {
+        if (lane == 0) {
+            int p = -1;
+            for (int r = col; r < e; ++r)
+                if (s_mat[r * w + col]) { p = r; break; }
+            s_piv = p;
+        }
+        __syncthreads();
+        const int p = s_piv;
+        if (p < 0) {  // singular: impossible for a Cauchy submatrix; flag and stop
+            if (lane == 0) a.e_out[g] = -1;
+            return;
+        }
+        if (p != col)
+            for (int c = lane; c < w; c += 64) {
+                const uint8_t t = s_mat[p * w + c];
+                s_mat[p * w + c] = s_mat[col * w + c];
+                s_mat[col * w + c] = t;
+            }
+        __syncthreads();
+        const uint32_t pv = s_mat[col * w + col];
+        const uint32_t pinv = s_exp[255 - s_log[pv]];
+        for (int c = lane; c < w; c += 64) s_mat[col * w + c] = static_cast<uint8_t>(gmul(s_mat[col * w + c], pinv));
+        __syncthreads();
+        for (int idx = lane; idx < e * w; idx += 64) {
+            const int r = idx / w, c = idx - r * w;
+            if (r == col) continue;
+            const uint32_t f = s_mat[r * w + col];
+            if (f && c != col) s_mat[r * w + c] ^= static_cast<uint8_t>(gmul(f, s_mat[col * w + c]));
+        }
+        __syncthreads();
+        for (int r = lane; r < e; r += 64)
+            if (r != col) s_mat[r * w + col] = 0;
+        __syncthreads();
+    }
+    uint8_t *Bc = a.coefB + static_cast<long long>(g) * a.coefB_gstride;
+    for (int l = 0; l < e; ++l)
+        for (int i = lane; i < a.ldB; i += 64)
+            Bc[static_cast<long long>(l) * a.ldB + i] = static_cast<uint8_t>(i < e ? s_mat[l * w + e + i] : 0);
+}
+
+// In-place finish of decode: recovered erasure l (dense scratch) goes to the l-th recovery block
+// of the group, whose row becomes erasure l. One thread per 4-byte word of the recovered data.
+__global__ __launch_bounds__(256) void scatter_recovered(ScatterArgs a) {
+    const int g = blockIdx.y;
+    const int e = a.e[g];
+    const int nw = (a.B + 3) / 4;
+    const long long t = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int l = static_cast<int>(t / nw);
+    const int w = static_cast<int>(t - static_cast<long long>(l) * nw);
+    if (l >= e) return;
+    const int j = a.rec_idx[static_cast<long long>(g) * a.emax + l];
+    const uint8_t *src = a.src + static_cast<long long>(g) * a.src_gstride + static_cast<long long>(l) * a.B + 4 * w;
+    uint8_t *dst = a.blocks + static_cast<long long>(g) * a.blocks_gstride + static_cast<long long>(j) * a.B + 4 * w;
+    const int nb = min(4, a.B - 4 * w);
+    if (nb == 4) st32(dst, ld32(src));
+    else for (int i = 0; i < nb; ++i) dst[i] = src[i];
+    if (w == 0) a.rows[static_cast<long long>(g) * a.rows_gstride + j] = a.erasures[static_cast<long long>(g) * a.emax + l];
+}
+
+// m == 1 decode (reference cauchy_decode_m1, cauchy_256.cpp:487-519): XOR every other block into
+// the first block with row >= k; its row is NOT rewritten. No such block -> untouched (the
+// reference reads past the array there). One thread per 4-byte word.
+__global__ __launch_bounds__(256) void decode_m1(uint8_t *blocks, long long blocks_gstride,
+                                                 const uint8_t *rows, long long rows_gstride, int k,
+                                                 int B, int groups) {
+    const int nw = (B + 3) / 4;
+    const long long t = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int g = static_cast<int>(t / nw);
+    const int w = static_cast<int>(t - static_cast<long long>(g) * nw);
+    if (g >= groups) return;
+    const uint8_t *r = rows + g * rows_gstride;
+    int er = -1;
+    for (int i = 0; i < k; ++i)
+        if (r[i] >= k) { er = i; break; }
+    if (er < 0) return;
+    uint8_t *base = blocks + g * blocks_gstride;
+    const int nb = min(4, B - 4 * w);
+    if (nb == 4) {
+        uint32_t x = ld32(base + static_cast<long long>(er) * B + 4 * w);
+        for (int i = 0; i < k; ++i)
+            if (i != er) x ^= ld32(base + static_cast<long long>(i) * B + 4 * w);
+        st32(base + static_cast<long long>(er) * B + 4 * w, x);
+    } else {
+        for (int bi = 0; bi < nb; ++bi) {
+            uint8_t x = base[static_cast<long long>(er) * B + 4 * w + bi];
+            for (int i = 0; i < k; ++i)
+                if (i != er) x ^= base[static_cast<long long>(i) * B + 4 * w + bi];
+            base[static_cast<long long>(er) * B + 4 * w + bi] = x;
+        }
+    }
+}
+
+// k <= 1 decode: blocks[0].row = 0 (cauchy_256.cpp:1236-1240).
+__global__ void decode_k1(uint8_t *rows, long long rows_gstride, int groups) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < groups) rows[g * rows_gstride] = 0;
+}
+
+// Synthetic workload (same stream as oracle/cauchy_oracle.c ora_fill_block): block x of group g
+// is PCG32 Seed(g*256 + x, cfg) output words, little-endian. One thread per block.
+__device__ __forceinline__ uint32_t pcg_next(uint64_t &state, uint64_t inc) {
+    const uint64_t old = state;
+    state = old * 6364136223846793005ull + inc;
+    const uint32_t xs = static_cast<uint32_t>(((old >> 18) ^ old) >> 27);
+    const uint32_t rot = static_cast<uint32_t>(old >> 59);
+    return (xs >> rot) | (xs << ((32u - rot) & 31u));
+}
+
+__global__ __launch_bounds__(256) void fill_pcg(uint8_t *out, long long gstride, int n, int B,
+                                                int groups, unsigned long long g0,
+                                                unsigned long long cfg) {
+    const long long t = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int g = static_cast<int>(t / n);
+    const int x = static_cast<int>(t - static_cast<long long>(g) * n);
+    if (g >= groups) return;
+    const uint64_t inc = (((g0 + g) * 256ull + x) << 1) | 1ull;
+    uint64_t state = 0;
+    pcg_next(state, inc);
+    state += cfg;
+    pcg_next(state, inc);
+    uint8_t *dst = out + g * gstride + static_cast<long long>(x) * B;
+    for (int p = 0; p < B; p += 4) {
+        const uint32_t v = pcg_next(state, inc);
+        if (p + 4 <= B) st32(dst + p, v);
+        else for (int i = 0; p + i < B; ++i) dst[p + i] = static_cast<uint8_t>(v >> (8 * i));
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Launch helpers (called from the host library; all asynchronous on `stream`).
+// ---------------------------------------------------------------------------------------------
+template <int R, bool PG>
+static hipError_t launch_apply_t(const ApplyArgs &a, hipStream_t stream) {
+    const int row_chunks = (a.n_out + R - 1) / R;
+    if (PG) {
+        dim3 grid((a.geo.nq + 63) / 64, row_chunks, a.groups);
+        hipLaunchKernelGGL((apply_generic<R, true>), grid, dim3(64), 0, stream, a);
+    } else {
+        const long long cols = static_cast<long long>(a.groups) * a.geo.nq;
+        dim3 grid(static_cast<unsigned>((cols + 255) / 256), row_chunks, 1);
+        hipLaunchKernelGGL((apply_generic<R, false>), grid, dim3(256), 0, stream, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_apply(const ApplyArgs &a, bool per_group, hipStream_t stream) {
+    if (a.n_out <= 0 || a.groups <= 0) return hipSuccess;
+    return per_group ? launch_apply_t<8, true>(a, stream) : launch_apply_t<8, false>(a, stream);
+}
+
+hipError_t launch_xor_rows(const uint8_t *in, long long in_gstride, int n_in, uint8_t *out,
+                           long long out_gstride, int B, int groups, hipStream_t stream) {
+    const long long n = static_cast<long long>(groups) * ((B + 3) / 4);
+    hipLaunchKernelGGL(xor_rows, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, stream,
+                       in, in_gstride, n_in, out, out_gstride, B, groups);
+    return hipGetLastError();
+}
+
+hipError_t launch_copy_first(const uint8_t *in, long long in_gstride, uint8_t *out,
+                             long long out_gstride, int m, int B, int groups, hipStream_t stream) {
+    const long long n = static_cast<long long>(groups) * m * B;
+    hipLaunchKernelGGL(copy_first, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, stream,
+                       in, in_gstride, out, out_gstride, m, B, groups);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode_setup(const DecodeSetupArgs &a, int groups, hipStream_t stream) {
+    hipLaunchKernelGGL(decode_setup, dim3(groups), dim3(64), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter(const ScatterArgs &a, int groups, hipStream_t stream) {
+    const long long n = static_cast<long long>(a.emax) * ((a.B + 3) / 4);
+    hipLaunchKernelGGL(scatter_recovered, dim3(static_cast<unsigned>((n + 255) / 256), groups),
+                       dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode_m1(uint8_t *blocks, long long blocks_gstride, const uint8_t *rows,
+                            long long rows_gstride, int k, int B, int groups, hipStream_t stream) {
+    const long long n = static_cast<long long>(groups) * ((B + 3) / 4);
+    hipLaunchKernelGGL(decode_m1, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, stream,
+                       blocks, blocks_gstride, rows, rows_gstride, k, B, groups);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode_k1(uint8_t *rows, long long rows_gstride, int groups, hipStream_t stream) {
+    hipLaunchKernelGGL(decode_k1, dim3((groups + 255) / 256), dim3(256), 0, stream, rows,
+                       rows_gstride, groups);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill(uint8_t *out, long long gstride, int n, int B, int groups,
+                       unsigned long long g0, unsigned long long cfg, hipStream_t stream) {
+    const long long t = static_cast<long long>(groups) * n;
+    hipLaunchKernelGGL(fill_pcg, dim3(static_cast<unsigned>((t + 255) / 256)), dim3(256), 0, stream,
+                       out, gstride, n, B, groups, g0, cfg);
+    return hipGetLastError();
+}
+
+}  // namespace sh

@@ -1,0 +1,92 @@
+// Device-side argument blocks and launch entry points (kernels.hip). Host code only sees plain
+// pointers and sizes; no torch types anywhere in the library.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sh {
+
+// Column geometry of a block size B (multiple of 8): sub = B/8 bytes per sub-block, nq 32-bit
+// word columns per sub-block, the last one holding `tail` (1..4) valid bytes.
+struct Geometry {
+    int B;
+    int sub;
+    int nq;
+    int tail;
+};
+
+inline Geometry make_geometry(int B) {
+    Geometry g;
+    g.B = B;
+    g.sub = B / 8;
+    g.nq = (g.sub + 3) / 4;
+    g.tail = g.sub - 4 * (g.nq - 1);
+    return g;
+}
+
+struct ApplyArgs {
+    const uint8_t *in;
+    long long in_gstride;   // bytes between groups
+    long long in_bstride;   // bytes between input blocks of a group
+    int n_in;
+    uint8_t *out;
+    long long out_gstride;
+    long long out_bstride;
+    int n_out;              // rows covered by the grid (max over groups)
+    const int *n_out_g;     // optional per-group row count (per-group mode)
+    const uint8_t *coef;    // coef[g*coef_gstride + o*coef_ld + j]; coef_ld % 4 == 0
+    long long coef_gstride; // 0 when shared by all groups
+    int coef_ld;
+    const uint64_t *rowbytes;  // 256 entries: byte b = c * 2^b in GF(256)/0x187
+    int groups;
+    Geometry geo;
+};
+
+struct DecodeSetupArgs {
+    int k, m;
+    const uint8_t *rows;    // [G][rows_gstride] block rows as handed in
+    long long rows_gstride;
+    const uint8_t *gen;     // (m-1) x k generator rows 1..m-1
+    const uint8_t *gf_exp;  // 512
+    const uint16_t *gf_log; // 256
+    int emax;
+    int *e_out;             // [G] erasure count (-1: singular)
+    uint8_t *rec_idx;       // [G][emax] array index of the i-th recovery block
+    uint8_t *erasures;      // [G][emax] i-th erased original row
+    uint8_t *coefA;         // [G][emax][ldA]
+    long long coefA_gstride;
+    int ldA;
+    uint8_t *coefB;         // [G][emax][ldB]
+    long long coefB_gstride;
+    int ldB;
+};
+
+struct ScatterArgs {
+    const uint8_t *src;     // [G][emax][B] recovered, dense
+    long long src_gstride;
+    uint8_t *blocks;        // [G][k][B] decode blocks, in place
+    long long blocks_gstride;
+    uint8_t *rows;          // [G][k]
+    long long rows_gstride;
+    const int *e;
+    const uint8_t *rec_idx;
+    const uint8_t *erasures;
+    int emax;
+    int B;
+};
+
+hipError_t launch_apply(const ApplyArgs &a, bool per_group, hipStream_t stream);
+hipError_t launch_xor_rows(const uint8_t *in, long long in_gstride, int n_in, uint8_t *out,
+                           long long out_gstride, int B, int groups, hipStream_t stream);
+hipError_t launch_copy_first(const uint8_t *in, long long in_gstride, uint8_t *out,
+                             long long out_gstride, int m, int B, int groups, hipStream_t stream);
+hipError_t launch_decode_setup(const DecodeSetupArgs &a, int groups, hipStream_t stream);
+hipError_t launch_scatter(const ScatterArgs &a, int groups, hipStream_t stream);
+hipError_t launch_decode_m1(uint8_t *blocks, long long blocks_gstride, const uint8_t *rows,
+                            long long rows_gstride, int k, int B, int groups, hipStream_t stream);
+hipError_t launch_decode_k1(uint8_t *rows, long long rows_gstride, int groups, hipStream_t stream);
+hipError_t launch_fill(uint8_t *out, long long gstride, int n, int B, int groups,
+                       unsigned long long g0, unsigned long long cfg, hipStream_t stream);
+
+}  // namespace sh

@@ -1,0 +1,266 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the reference's golden vectors, the
+oracle, and size-independent properties at BASELINE.json's full sizes. Bit-exact everywhere
+(integer/byte arithmetic: no tolerance)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as po
+from tests.golden_util import case_inputs, manifest, sha, vectors
+
+pytestmark = pytest.mark.gpu
+CASES = manifest()
+
+
+@pytest.fixture(scope="module")
+def sh():
+    import torch
+    import shorthair_amd
+    assert shorthair_amd.cauchy_256_init() == 0
+    torch.cuda.init()
+    return shorthair_amd
+
+
+def _dev(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _sync():
+    import torch
+    torch.cuda.synchronize()
+
+
+# ------------------------------------------------------------------------- golden vectors
+@pytest.mark.parametrize("c", [c for c in CASES if c["kind"] == "encode"], ids=lambda c: c["name"])
+def test_encode_batch_golden(sh, c):
+    import torch
+    k, m, B = c["k"], c["m"], c["B"]
+    data, _ = case_inputs(po, c)
+    d_in = _dev(data[None])
+    d_out = torch.zeros((1, m, B), dtype=torch.uint8, device="cuda")
+    rc = sh.encode_batch(k, m, B, 1, d_in, d_out)
+    _sync()
+    assert rc == c["rc"]
+    out = d_out[0].cpu().numpy()
+    assert sha(out) == c["out_sha"]
+    if c["full"]:
+        assert np.array_equal(out, vectors()[c["name"] + "_out"])
+
+
+@pytest.mark.parametrize("c", [c for c in CASES if c["kind"] == "decode"], ids=lambda c: c["name"])
+def test_decode_batch_golden(sh, c):
+    k, m, B = c["k"], c["m"], c["B"]
+    data, rows = case_inputs(po, c)
+    _, rec = po.oracle().encode(k, m, data, B)
+    whole = np.concatenate([data, rec])
+    blocks = np.stack([whole[r] for r in rows])
+    assert sha(blocks) == c["in_sha"]
+    d_blocks, d_rows = _dev(blocks[None]), _dev(rows[None])
+    rc = sh.decode_batch(k, m, B, 1, d_blocks, d_rows)
+    _sync()
+    assert rc == c["rc"]
+    assert d_rows[0].cpu().numpy().tolist() == c["rows_out"]
+    out = d_blocks[0].cpu().numpy()
+    assert sha(out) == c["out_sha"]
+    if c["full"]:
+        assert np.array_equal(out, vectors()[c["name"] + "_out"])
+
+
+# ------------------------------------------------------------------------- drop-in single-group ABI
+@pytest.mark.parametrize("c", [c for c in CASES if c["kind"] == "encode" and c["full"]],
+                         ids=lambda c: c["name"])
+def test_single_group_encode_abi_misaligned(sh, c):
+    """cauchy_256_encode on host pointers misaligned like Shorthair's (p->data + 3)."""
+    k, m, B = c["k"], c["m"], c["B"]
+    data, _ = case_inputs(po, c)
+    raw = np.zeros(k * (B + 16) + 64, np.uint8)
+    ptrs = []
+    for x in range(k):
+        off = 3 + x * (B + 16)
+        raw[off:off + B] = data[x]
+        ptrs.append(raw.ctypes.data + off)
+    rec_raw = np.zeros(m * B + 8, np.uint8)
+    rc = sh.cauchy_256_encode(k, m, ptrs, rec_raw.ctypes.data + 5, B)
+    assert rc == c["rc"]
+    out = rec_raw[5:5 + m * B].reshape(m, B)
+    assert np.array_equal(out, vectors()[c["name"] + "_out"])
+
+
+@pytest.mark.parametrize("c", [c for c in CASES if c["kind"] == "decode" and c["full"]],
+                         ids=lambda c: c["name"])
+def test_single_group_decode_abi(sh, c):
+    k, m, B = c["k"], c["m"], c["B"]
+    data, rows = case_inputs(po, c)
+    _, rec = po.oracle().encode(k, m, data, B)
+    whole = np.concatenate([data, rec])
+    bufs = [np.concatenate([np.zeros(1, np.uint8), whole[r]]) for r in rows]  # +1 misalign
+    arr = (sh.Block * k)()
+    for i in range(k):
+        arr[i].data = bufs[i].ctypes.data + 1
+        arr[i].row = int(rows[i])
+    rc = sh.cauchy_256_decode(k, m, arr, B)
+    assert rc == c["rc"]
+    assert [arr[i].row for i in range(k)] == c["rows_out"]
+    out = np.stack([b[1:] for b in bufs])
+    assert np.array_equal(out, vectors()[c["name"] + "_out"])
+
+
+# ------------------------------------------------------------------------- batches vs oracle
+def _oracle_encode_groups(k, m, B, cfg, groups):
+    ora = po.oracle()
+    res = {}
+    for g in groups:
+        data = po.fill_group(g, k, B, cfg)
+        rc, out = ora.encode(k, m, data, B)
+        assert rc == 0
+        res[g] = (data, out)
+    return res
+
+
+@pytest.mark.parametrize("k,m,B,G", [(64, 16, 1400, 4096), (28, 4, 256, 512), (112, 16, 1400, 300),
+                                     (224, 32, 65536, 8), (200, 32, 1400, 1024), (2, 2, 8, 1000),
+                                     (250, 6, 16, 64), (13, 9, 24, 333)])
+def test_encode_batch_vs_oracle(sh, k, m, B, G):
+    """BASELINE configs[1] (4096 x k=64 m=16 1400B) and sweep shapes: device-generated input
+    equals the oracle's generator (sha of a sample), encode bit-exact on sampled groups."""
+    import torch
+    cfg = 0xC2 + k
+    d_in = torch.empty((G, k, B), dtype=torch.uint8, device="cuda")
+    d_out = torch.empty((G, m, B), dtype=torch.uint8, device="cuda")
+    assert sh.fill_synthetic(d_in, k, B, G, 0, cfg) == 0
+    assert sh.encode_batch(k, m, B, G, d_in, d_out) == 0
+    _sync()
+    sample = sorted({0, 1, G // 2, G - 2, G - 1})
+    exp = _oracle_encode_groups(k, m, B, cfg, sample)
+    for g in sample:
+        assert np.array_equal(d_in[g].cpu().numpy(), exp[g][0]), f"input g={g}"
+        assert np.array_equal(d_out[g].cpu().numpy(), exp[g][1]), f"recovery g={g}"
+
+
+def test_encode_manifest_big_shapes(sh):
+    """Digests of the reference on the C2/C3/C4 shapes (tests/golden/manifest.json big_enc_*)."""
+    import torch
+    for c in [c for c in CASES if c["kind"] == "encode" and c["name"].startswith("big_")]:
+        k, m, B = c["k"], c["m"], c["B"]
+        d_in = torch.empty((1, k, B), dtype=torch.uint8, device="cuda")
+        d_out = torch.empty((1, m, B), dtype=torch.uint8, device="cuda")
+        sh.fill_synthetic(d_in, k, B, 1, c["g"], c["cfg"])
+        assert sh.encode_batch(k, m, B, 1, d_in, d_out) == 0
+        _sync()
+        assert sha(d_in[0].cpu().numpy()) == c["in_sha"], c["name"]
+        assert sha(d_out[0].cpu().numpy()) == c["out_sha"], c["name"]
+
+
+def _decode_inputs(k, m, B, G, cfg, e_fixed):
+    """Device-resident decode batch: encode on the GPU, then gather each group's received blocks
+    in the order of its (oracle-generated) erasure pattern."""
+    import torch
+    data = torch.empty((G, k, B), dtype=torch.uint8, device="cuda")
+    rec = torch.empty((G, m, B), dtype=torch.uint8, device="cuda")
+    assert __import__("shorthair_amd").fill_synthetic(data, k, B, G, 0, cfg) == 0
+    assert __import__("shorthair_amd").encode_batch(k, m, B, G, data, rec) == 0
+    rows = np.zeros((G, k), np.uint8)
+    es = np.zeros(G, np.int64)
+    for g in range(G):
+        es[g], rows[g] = po.erasure_pattern(g, k, m, cfg, e_fixed)
+    d_rows = torch.from_numpy(rows).cuda()
+    whole = torch.cat([data, rec], dim=1)
+    idx = d_rows.long()
+    blocks = whole[torch.arange(G, device="cuda")[:, None], idx].contiguous()
+    del whole
+    return data, rec, blocks, d_rows, rows, es
+
+
+@pytest.mark.parametrize("k,m,B,G,e_fixed", [(200, 32, 1400, 8192, 0), (200, 32, 1400, 2048, 32),
+                                             (64, 16, 1400, 1024, 0), (28, 4, 256, 700, 0),
+                                             (112, 16, 65536, 6, 0), (128, 128, 8, 64, 0),
+                                             (30, 9, 48, 500, 9)])
+def test_decode_batch_roundtrip_and_oracle(sh, k, m, B, G, e_fixed):
+    """BASELINE configs[2] (8192 x k=200 m=32 1400B, random erasures up to 32): every group's
+    recovered blocks equal the erased originals (encode -> erase -> decode round trip, whole
+    batch), the row rewrite follows the reference contract, and sampled groups match the oracle
+    byte for byte."""
+    import torch
+    cfg = 0xD3 + k
+    data, rec, blocks, d_rows, rows, es = _decode_inputs(k, m, B, G, cfg, e_fixed)
+    orig_blocks = blocks.clone()
+    assert sh.decode_batch(k, m, B, G, blocks, d_rows) == 0
+    _sync()
+    new_rows = d_rows.cpu().numpy()
+    # rows: originals unchanged, recovery blocks -> erasures ascending in array order
+    for g in range(0, G, max(1, G // 64)):
+        present = set(int(r) for r in rows[g] if r < k)
+        missing = [x for x in range(k) if x not in present]
+        rec_pos = [i for i in range(k) if rows[g][i] >= k]
+        exp = rows[g].copy()
+        for i, p in enumerate(rec_pos):
+            exp[p] = missing[i]
+        assert np.array_equal(new_rows[g], exp), g
+    # data: every block equals original data[row] (whole batch, on device)
+    idx = torch.from_numpy(new_rows).cuda().long()
+    truth = data[torch.arange(G, device="cuda")[:, None], idx]
+    assert torch.equal(blocks, truth)
+    # sampled groups vs the oracle's own decode
+    ora = po.oracle()
+    for g in sorted({0, G // 3, G - 1}):
+        b = [x.copy() for x in orig_blocks[g].cpu().numpy()]
+        rc, nr = ora.decode(k, m, b, list(rows[g]), B)
+        assert rc == 0 and nr == new_rows[g].tolist()
+        assert np.array_equal(np.stack(b), blocks[g].cpu().numpy())
+
+
+def test_decode_batch_out_matches_inplace(sh):
+    import torch
+    k, m, B, G = 200, 32, 1400, 512
+    data, rec, blocks, d_rows, rows, es = _decode_inputs(k, m, B, G, 0xAB, 0)
+    emax = min(k, m)
+    out = torch.zeros((G, emax, B), dtype=torch.uint8, device="cuda")
+    out_rows = torch.zeros((G, emax), dtype=torch.uint8, device="cuda")
+    out_cnt = torch.zeros(G, dtype=torch.int32, device="cuda")
+    assert sh.decode_batch_out(k, m, B, G, blocks, d_rows, out, out_rows, out_cnt) == 0
+    _sync()
+    cnt = out_cnt.cpu().numpy()
+    assert np.array_equal(cnt, es)
+    orow = out_rows.cpu().numpy()
+    for g in range(G):
+        e = int(cnt[g])
+        truth = data[g, torch.from_numpy(orow[g, :e]).long().cuda()]
+        assert torch.equal(out[g, :e], truth), g
+
+
+def test_decode_no_erasures_and_invalid(sh):
+    """Groups with nothing erased are untouched; invalid parameters return -1 only when some
+    group has something to recover (reference cauchy_256.cpp:1266-1273)."""
+    import torch
+    k, m, B, G = 20, 4, 64, 5
+    blocks = torch.randint(0, 256, (G, k, B), dtype=torch.uint8, device="cuda")
+    rows = torch.arange(k, dtype=torch.uint8, device="cuda").repeat(G, 1).contiguous()
+    before = blocks.clone()
+    assert sh.decode_batch(k, m, B, G, blocks, rows) == 0
+    _sync()
+    assert torch.equal(blocks, before)
+    assert sh.decode_batch(k, m, 12, G, blocks, rows) == 0  # B % 8 != 0 but nothing to do
+    rows2 = rows.clone()
+    rows2[1, 3] = k + 1
+    assert sh.decode_batch(k, m, 12, G, blocks, rows2) == -1
+    assert sh.decode_batch(200, 60, 16, 1, torch.zeros((1, 200, 16), dtype=torch.uint8, device="cuda"),
+                           torch.full((1, 200), 200, dtype=torch.uint8, device="cuda")) == -1
+
+
+def test_tiny_and_odd_block_sizes(sh):
+    """B = 8/16/24 (sub-blocks shorter than a word) and B % 32 != 0 tails, encode + decode."""
+    ora = po.oracle()
+    rng = np.random.default_rng(7)
+    import torch
+    for B in (8, 16, 24, 40, 56, 1352, 1336, 1344, 4104):
+        k, m = 17, 5
+        G = 9
+        data = rng.integers(0, 256, (G, k, B), dtype=np.uint8)
+        d_out = torch.zeros((G, m, B), dtype=torch.uint8, device="cuda")
+        assert sh.encode_batch(k, m, B, G, _dev(data), d_out) == 0
+        _sync()
+        for g in range(G):
+            _, exp = ora.encode(k, m, data[g], B)
+            assert np.array_equal(d_out[g].cpu().numpy(), exp), (B, g)
