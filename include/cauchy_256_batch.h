@@ -4,7 +4,8 @@
  * The reference codes one group per call on one CPU thread (cauchy_256.cpp:1479, :1233). Here a
  * call codes `groups` independent code groups that already sit in GPU memory (HBM), with the same
  * per-group semantics and bytes as cauchy_256_encode / cauchy_256_decode. All calls are
- * asynchronous on `stream` (a hipStream_t, NULL = the library's stream) and enqueue no host
+ * asynchronous on `stream` (a hipStream_t passed through verbatim: NULL = the null stream) and
+ * enqueue no host
  * synchronisation, except where noted for invalid parameters.
  *
  * Layouts (byte offsets inside one device allocation, no alignment required):
@@ -53,7 +54,8 @@ int cauchy_256_batch_reserve(int k, int m, int block_bytes, int groups);
 int cauchy_256_fill_synthetic(void *d_out, int n, int block_bytes, int groups,
                               unsigned long long g0, unsigned long long cfg, void *stream);
 
-/* Library's own stream (hipStream_t) and a device synchronize helper for callers without HIP. */
+/* The library's private stream (used by the single-group calls) and a synchronize helper for
+ * callers without HIP. */
 void *cauchy_256_default_stream(void);
 int cauchy_256_sync(void *stream);
 

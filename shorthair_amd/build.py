@@ -12,27 +12,68 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libcauchy256.so")
-SOURCES = ["kernels.hip", "cauchy_256_host.cpp"]
+SOURCES = ["kernels.hip", "fixed_dispatch.cpp", "cauchy_256_host.cpp"]
+GEN_DIR = os.path.join(CSRC, "gen")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SH_OFFLOAD_ARCH", "gfx950")
+
+
+def _gen_sources():
+    return sorted(os.path.join(GEN_DIR, f) for f in os.listdir(GEN_DIR) if f.endswith(".hip"))
 
 
 def _stale():
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if os.path.isfile(os.path.join(CSRC, f))]
+    deps += [os.path.join(GEN_DIR, f) for f in os.listdir(GEN_DIR)]
     deps += [os.path.join(HERE, "..", "include", f) for f in os.listdir(os.path.join(HERE, "..", "include"))]
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=True):
+FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result"]
+OBJ_DIR = os.path.join(HERE, "build_obj")
+
+
+def _compile(src, verbose):
+    obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
+    if os.path.exists(obj) and os.path.getmtime(obj) >= max(
+            os.path.getmtime(src), os.path.getmtime(os.path.join(CSRC, "fixed_common.hpp")),
+            os.path.getmtime(os.path.join(CSRC, "kernels.hpp"))):
+        return obj, None
+    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    return obj, subprocess.Popen(cmd)
+
+
+def build(force=False, verbose=True, jobs=None):
+    """Compile every source to build_obj/ (generated kernels in parallel: each is a large
+    straight-line function, ~1-2 min for k=200) and link libcauchy256.so."""
     if not force and not _stale():
         return LIB
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-result",
-           f"-Wl,--version-script={os.path.join(CSRC, 'exports.map')}",
-           "-o", LIB + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    if force:
+        for f in os.listdir(OBJ_DIR):
+            os.remove(os.path.join(OBJ_DIR, f))
+    jobs = jobs or max(1, min(8, os.cpu_count() or 1))
+    srcs = _gen_sources() + [os.path.join(CSRC, s) for s in SOURCES]
+    objs, running = [], []
+    for src in srcs:
+        while len(running) >= jobs:
+            p = running.pop(0)
+            if p.wait() != 0:
+                raise subprocess.CalledProcessError(p.returncode, p.args)
+        obj, p = _compile(src, verbose)
+        objs.append(obj)
+        if p is not None:
+            running.append(p)
+    for p in running:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, p.args)
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC",
+           f"-Wl,--version-script={os.path.join(CSRC, 'exports.map')}", "-o", LIB + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

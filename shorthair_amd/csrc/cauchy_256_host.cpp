@@ -145,8 +145,35 @@ uint8_t *generator(Context &c, int k, int m) {
     return d;
 }
 
-hipStream_t pick(void *stream) {
-    return stream ? static_cast<hipStream_t>(stream) : ctx().stream;
+// Batched calls take the caller's stream verbatim (NULL = the null stream, as in HIP itself).
+hipStream_t pick(void *stream) { return static_cast<hipStream_t>(stream); }
+
+// Compile-time-scheduled kernels address one launch's input/output with 32-bit buffer offsets:
+// split the batch so every launch spans < 2 GiB on each side.
+hipError_t launch_fixed_chunked(int k, int m, int B, int groups, const uint8_t *in, long long in_gs,
+                                uint8_t *out, long long out_gs, const uint8_t *pos,
+                                const uint8_t *rpos, bool dec, hipStream_t s) {
+    const long long limit = (1ll << 31) - (1ll << 24);
+    const long long per = std::max(in_gs, out_gs);
+    const int chunk = static_cast<int>(std::max(1ll, std::min<long long>(groups, limit / per)));
+    const int KP = round4(k), MP = round4(m);
+    for (int g0 = 0; g0 < groups; g0 += chunk) {
+        sh::FixedArgs a{};
+        const int n = std::min(chunk, groups - g0);
+        a.in = in + g0 * in_gs;
+        a.in_gstride = in_gs;
+        a.in_bytes = n * in_gs;
+        a.out = out + g0 * out_gs;
+        a.out_gstride = out_gs;
+        a.out_bytes = n * out_gs;
+        a.groups = n;
+        a.geo = sh::make_geometry(B);
+        a.pos = pos ? pos + static_cast<long long>(g0) * KP : nullptr;
+        a.rpos = rpos ? rpos + static_cast<long long>(g0) * MP : nullptr;
+        hipError_t e = sh::launch_fixed(k, m, a, dec, s);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 // ---- batched encode ----
@@ -165,7 +192,11 @@ int encode_batch(int k, int m, int B, int groups, const uint8_t *d_in, uint8_t *
         // Row 0 (plain XOR, any B) is written even when the parameters are then rejected
         // (reference cauchy_256.cpp:1496-1511).
         SH_CHECK(sh::launch_xor_rows(d_in, in_gs, k, d_out, out_gs, B, groups, s));
-        return valid ? 0 : -1;
+        return (m == 1 || valid) ? 0 : -1;  // m == 1 returns before validation (:1503-1506)
+    }
+    if (sh::has_fixed(k, m, B)) {
+        SH_CHECK(launch_fixed_chunked(k, m, B, groups, d_in, in_gs, d_out, out_gs, nullptr, nullptr, false, s));
+        return 0;
     }
     uint8_t *gen = generator(c, k, m);
     if (!gen) return -2;
@@ -191,16 +222,19 @@ int encode_batch(int k, int m, int B, int groups, const uint8_t *d_in, uint8_t *
 
 // Workspace carve for decode of `groups` groups.
 struct DecodeWS {
-    int emax, ldA, ldB;
+    bool fixed;       // stage A by a compile-time-scheduled kernel (has_fixed(k, m, B))
+    int emax, ldA, ldB, nres;  // nres: residual rows per group (m when fixed, else emax)
     int *e;
-    uint8_t *rec_idx, *erasures, *coefA, *coefB, *residual, *recovered;
+    uint8_t *rec_idx, *erasures, *coefA, *coefB, *residual, *recovered, *pos, *rpos;
     long long coefA_gs, coefB_gs;
 };
 
 size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool need_recovered) {
+    w.fixed = sh::has_fixed(k, m, B);
     w.emax = std::min(k, m);
-    w.ldA = round4(k);
-    w.ldB = round4(w.emax);
+    w.ldA = w.fixed ? 0 : round4(k);
+    w.ldB = w.fixed ? round4(m) : round4(w.emax);
+    w.nres = w.fixed ? m : w.emax;
     w.coefA_gs = static_cast<long long>(w.emax) * w.ldA;
     w.coefB_gs = static_cast<long long>(w.emax) * w.ldB;
     size_t off = 0;
@@ -213,9 +247,11 @@ size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool n
     w.e = reinterpret_cast<int *>(take(G * sizeof(int)));
     w.rec_idx = take(G * w.emax);
     w.erasures = take(G * w.emax);
-    w.coefA = take(G * w.coefA_gs);
+    w.coefA = w.fixed ? nullptr : take(G * w.coefA_gs);
     w.coefB = take(G * w.coefB_gs);
-    w.residual = take(G * w.emax * static_cast<size_t>(B));
+    w.pos = w.fixed ? take(G * round4(k)) : nullptr;
+    w.rpos = w.fixed ? take(G * round4(m)) : nullptr;
+    w.residual = take(G * w.nres * static_cast<size_t>(B));
     w.recovered = need_recovered ? take(G * w.emax * static_cast<size_t>(B)) : nullptr;
     return off;
 }
@@ -244,9 +280,36 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
     sa.coefB = w.coefB;
     sa.coefB_gstride = w.coefB_gs;
     sa.ldB = w.ldB;
+    sa.pos = w.pos;
+    sa.rpos = w.rpos;
     SH_CHECK(sh::launch_decode_setup(sa, groups, s));
 
     const Geometry geo = sh::make_geometry(B);
+    if (w.fixed) {
+        // Stage A (compile-time generator, all m rows, erased columns read as zeros):
+        //   residual_y = R_y + sum_{received x} M(C[y][x]) d_x
+        SH_CHECK(launch_fixed_chunked(k, m, B, groups, d_blocks, static_cast<long long>(k) * B,
+                                      w.residual, static_cast<long long>(m) * B, w.pos, w.rpos, true, s));
+        // Stage B: recovered_l = sum_y M(coefB[l][y]) residual_y  (coefB = S^-1 on received rows)
+        sh::ApplyArgs b{};
+        b.in = w.residual;
+        b.in_gstride = static_cast<long long>(m) * B;
+        b.in_bstride = B;
+        b.n_in = m;
+        b.out = dst;
+        b.out_gstride = static_cast<long long>(w.emax) * B;
+        b.out_bstride = B;
+        b.n_out = w.emax;
+        b.n_out_g = w.e;
+        b.coef = w.coefB;
+        b.coef_gstride = w.coefB_gs;
+        b.coef_ld = w.ldB;
+        b.rowbytes = c.d_rowbytes;
+        b.groups = groups;
+        b.geo = geo;
+        SH_CHECK(sh::launch_apply(b, true, s));
+        return 0;
+    }
     // Stage A: residual_i = R_i + sum_{orig j} M(C[r_i][row_j]) d_j  (per-group coefficients)
     sh::ApplyArgs a{};
     a.in = d_blocks;

@@ -298,9 +298,23 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
         return r == 0 ? 1u : a.gen[static_cast<long long>(r - 1) * k + x];
     };
 
+    const bool fixed_mode = (a.coefA == nullptr);
+    if (fixed_mode) {
+        const int KP = (k + 3) & ~3, MP = (a.m + 3) & ~3;
+        uint8_t *pos = a.pos + static_cast<long long>(g) * KP;
+        uint8_t *rpos = a.rpos + static_cast<long long>(g) * MP;
+        for (int x = lane; x < KP; x += 64) pos[x] = 0xFF;
+        for (int y = lane; y < MP; y += 64) rpos[y] = 0xFF;
+        __syncthreads();
+        for (int j = lane; j < k; j += 64) {
+            const int row = s_rows[j];
+            if (row < k) pos[row] = static_cast<uint8_t>(j);
+            else if (row - k < a.m) rpos[row - k] = static_cast<uint8_t>(j);
+        }
+    }
     // Stage-A coefficients, row-major [i][j], leading dimension ldA.
-    uint8_t *A = a.coefA + static_cast<long long>(g) * a.coefA_gstride;
-    for (int i = 0; i < e; ++i) {
+    uint8_t *A = fixed_mode ? nullptr : a.coefA + static_cast<long long>(g) * a.coefA_gstride;
+    for (int i = 0; i < e && !fixed_mode; ++i) {
         const int r = s_rrow[i];
         for (int j = lane; j < a.ldA; j += 64) {
             uint32_t c = 0;
@@ -354,9 +368,19 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
         __syncthreads();
     }
     uint8_t *Bc = a.coefB + static_cast<long long>(g) * a.coefB_gstride;
-    for (int l = 0; l < e; ++l)
-        for (int i = lane; i < a.ldB; i += 64)
-            Bc[static_cast<long long>(l) * a.ldB + i] = static_cast<uint8_t>(i < e ? s_mat[l * w + e + i] : 0);
+    if (fixed_mode) {
+        // coefB[l][y] = S^-1[l][i] where r_i = y; zero for rows that were not received
+        for (int l = 0; l < e; ++l) {
+            for (int y = lane; y < a.ldB; y += 64) Bc[static_cast<long long>(l) * a.ldB + y] = 0;
+            __syncthreads();
+            for (int i = lane; i < e; i += 64) Bc[static_cast<long long>(l) * a.ldB + s_rrow[i]] = s_mat[l * w + e + i];
+            __syncthreads();
+        }
+    } else {
+        for (int l = 0; l < e; ++l)
+            for (int i = lane; i < a.ldB; i += 64)
+                Bc[static_cast<long long>(l) * a.ldB + i] = static_cast<uint8_t>(i < e ? s_mat[l * w + e + i] : 0);
+    }
 }
 
 // In-place finish of decode: recovered erasure l (dense scratch) goes to the l-th recovery block

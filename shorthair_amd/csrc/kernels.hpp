@@ -60,6 +60,11 @@ struct DecodeSetupArgs {
     uint8_t *coefB;         // [G][emax][ldB]
     long long coefB_gstride;
     int ldB;
+    // Fixed-kernel mode (coefA == nullptr): stage A runs the compile-time generator over all m
+    // rows, so the setup emits position tables instead of stage-A coefficients, and stage B's
+    // coefficients are indexed by generator row y (coefB[l][y], ldB >= m) rather than by i.
+    uint8_t *pos;           // [G][round4(k)] array index of original row x (0xFF = erased)
+    uint8_t *rpos;          // [G][round4(m)] array index of recovery row y (0xFF = absent)
 };
 
 struct ScatterArgs {
@@ -75,6 +80,27 @@ struct ScatterArgs {
     int emax;
     int B;
 };
+
+// Compile-time-scheduled kernels (csrc/gen/, tools/gen_fixed_kernels.py).
+struct FixedArgs {
+    const uint8_t *in;        // encode: data [G][k][B]; decode A: received blocks [G][k][B]
+    long long in_gstride;
+    long long in_bytes;       // groups * in_gstride (< 2 GiB per launch; the host splits)
+    uint8_t *out;             // encode: recovery [G][m][B]; decode A: residual [G][m][B]
+    long long out_gstride;
+    long long out_bytes;      // groups * out_gstride (< 2 GiB per launch)
+    int groups;
+    Geometry geo;
+    const uint8_t *pos;       // decode: [G][round4(k)] array index of original row x, 0xFF = erased
+    const uint8_t *rpos;      // decode: [G][round4(m)] array index of recovery row y, 0xFF = absent
+    const uint8_t *zero;      // decode: >= B zero bytes
+    int groups_per_wg;        // set by the launcher
+};
+
+// Returns hipErrorNotSupported (and launches nothing) when (k, m) has no generated kernel or the
+// block is too short (sub < 4).
+hipError_t launch_fixed(int k, int m, FixedArgs a, bool dec, hipStream_t stream);
+bool has_fixed(int k, int m, int B);
 
 hipError_t launch_apply(const ApplyArgs &a, bool per_group, hipStream_t stream);
 hipError_t launch_xor_rows(const uint8_t *in, long long in_gstride, int n_in, uint8_t *out,

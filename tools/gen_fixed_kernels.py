@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""Generate compile-time-scheduled bitmatrix kernels: shorthair_amd/csrc/gen/fixed_k<k>_m<m>.hip.
+
+For a fixed (k, m) the generator matrix is a constant (reference cauchy_matrix(),
+cauchy_256.cpp:423-481, depends only on k and m), so every XOR of the windowed bitmatrix product
+(reference win_encode, cauchy_256.cpp:1398-1477) can be scheduled at build time: the table index
+of each lookup becomes a register name instead of a runtime value. That turns each output
+sub-block row update into ONE v_bitop3_b32 (a ^ T0[lo] ^ T1[hi]) with no index arithmetic --
+measured 8.7x cheaper than hipcc's s_set_gpr_idx lowering of a runtime-indexed table.
+Every XOR is emitted as a bitop3 intrinsic (X2 = truth table 0x3C for a 2-input XOR): plain `^`
+chains spanning all k steps are reassociated by LLVM into trees that keep every loaded word live
+(256 VGPRs + AGPR spills even at k=28).
+
+One generated kernel serves two modes (template flag DEC):
+  encode       recovery[g][y] = sum_x M(C[y][x]) data[g][x]             (y < m, row 0 = ones)
+  decode A     residual[g][y] = R_y + sum_{x received} M(C[y][x]) d_x   (erased x read as zeros)
+Rows are split into parts of <= 16 rows (128 accumulator VGPRs); the waves of one workgroup
+run the parts of the same columns, so the second part's loads hit L1/L2.
+
+Usage: python tools/gen_fixed_kernels.py            (all configs in CONFIGS)
+"""
+import os
+import sys
+
+ROOT = os.path.normpath(os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, ROOT)
+OUTDIR = os.path.join(ROOT, "shorthair_amd", "csrc", "gen")
+
+# (k, m): BASELINE.json configs -- headline (200,32), C2 (64,16), C4 sweep (28,4),(112,16),(224,32)
+CONFIGS = [(200, 32), (64, 16), (28, 4), (112, 16), (224, 32)]
+ROWS_PER_PART = 16
+
+
+def gf_tables():
+    exp = [0] * 512
+    log = [0] * 256
+    x = 1
+    for i in range(255):
+        exp[i] = exp[i + 255] = x
+        log[x] = i
+        x <<= 1
+        if x & 0x100:
+            x ^= 0x187
+    return exp, log
+
+
+EXP, LOG = gf_tables()
+
+
+def gmul(a, b):
+    return 0 if a == 0 or b == 0 else EXP[LOG[a] + LOG[b]]
+
+
+def generator(k, m):
+    """Full m x k generator (row 0 = ones) from the oracle's restatement of cauchy_matrix()."""
+    from oracle import pyoracle as po
+    rows = [[1] * k]
+    if m >= 2:
+        mat = po.cauchy_matrix(k, m)
+        rows += [list(map(int, mat[y])) for y in range(m - 1)]
+    return rows
+
+
+def row_bytes(c):
+    out = []
+    for _ in range(8):
+        out.append(c)
+        c = gmul(c, 2)
+    return out
+
+
+class Body:
+    """Straight-line code for one part (rows y0..y1-1) over all k inputs."""
+
+    def __init__(self, k, rows, y0, y1):
+        self.k, self.rows, self.y0, self.y1 = k, rows, y0, y1
+        self.lines = []
+
+    def table_expr(self, h, v, have):
+        """Name of window-table entry v (1..15) of half h, building it if needed."""
+        base = {1: f"d{4*h+0}", 2: f"d{4*h+1}", 4: f"d{4*h+2}", 8: f"d{4*h+3}"}
+        if v in base:
+            return base[v]
+        name = f"t{h}_{v}"
+        if name in have:
+            return name
+        bits = [b for b in (1, 2, 4, 8) if v & b]
+        if len(bits) == 2:
+            self.lines.append(f"    const uint32_t {name} = X2({base[bits[0]]}, {base[bits[1]]});")
+        elif len(bits) == 3:
+            self.lines.append(f"    const uint32_t {name} = X3({base[bits[0]]}, {base[bits[1]]}, {base[bits[2]]});")
+        else:  # 15 = 3 ^ 12
+            a = self.table_expr(h, 3, have)
+            b = self.table_expr(h, 12, have)
+            self.lines.append(f"    const uint32_t {name} = X2({a}, {b});")
+        have.add(name)
+        return name
+
+    def emit(self, pf=2):
+        """Inputs are prefetched `pf` steps ahead into a ring of register sets (raw words; the
+        only per-step fix-up is Src::fix7 for the buffer-end tail lane)."""
+        L = self.lines
+        nr = self.y1 - self.y0
+        for s in range(pf):
+            L.append(f"    uint32_t r{s}_0, r{s}_1, r{s}_2, r{s}_3, r{s}_4, r{s}_5, r{s}_6, r{s}_7;")
+        L.append("    uint32_t d0, d1, d2, d3, d4, d5, d6, d7;")
+        for s in range(min(pf, self.k)):
+            L.append(f"    src.load({s}, " + ", ".join(f"r{s}_{a}" for a in range(8)) + ");")
+        for x in range(self.k):
+            slot = x % pf
+            L.append(f"    // ---- input block {x}")
+            # Pin the step structure: without this hipcc hoists all k steps' loads and address
+            # arithmetic to the top (256 VGPRs + spills, 1 wave/SIMD).
+            L.append("    __builtin_amdgcn_sched_barrier(0);")
+            L.append("    " + " ".join(f"d{a} = r{slot}_{a};" for a in range(8)))
+            L.append(f"    d7 = src.fix7({x}, d7);")
+            if x + pf < self.k:
+                L.append(f"    src.load({x + pf}, " + ", ".join(f"r{slot}_{a}" for a in range(8)) + ");")
+            L.append("    {")
+            have = set()
+            for yi in range(nr):
+                c = self.rows[self.y0 + yi][x]
+                for b, v in enumerate(row_bytes(c)):
+                    lo, hi = v & 15, v >> 4
+                    acc = f"acc[{yi}][{b}]"
+                    if lo and hi:
+                        ta = self.table_expr(0, lo, have)
+                        tb = self.table_expr(1, hi, have)
+                        L.append(f"    {acc} = X3({acc}, {ta}, {tb});")
+                    elif lo:
+                        L.append(f"    {acc} = X2({acc}, {self.table_expr(0, lo, have)});")
+                    else:
+                        L.append(f"    {acc} = X2({acc}, {self.table_expr(1, hi, have)});")
+            # Tie every accumulator to this step (an empty volatile asm is a chained side effect):
+            # otherwise the DAG scheduler floats the pure bitop3 nodes of a ~30K-node basic block
+            # away from their loads and keeps every loaded word live.
+            for yi in range(nr):
+                L.append(f"    PIN8(acc[{yi}]);")
+            L.append("    }")
+        return "\n".join(L)
+
+
+def gen_config(k, m):
+    rows = generator(k, m)
+    parts = [(y0, min(m, y0 + ROWS_PER_PART)) for y0 in range(0, m, ROWS_PER_PART)]
+    name = f"k{k}_m{m}"
+    out = [f"// GENERATED by tools/gen_fixed_kernels.py -- do not edit. (k={k}, m={m})",
+           "// Compile-time-scheduled windowed bitmatrix product for one generator; see the",
+           "// generator's docstring and DESIGN.md.",
+           '#include "../fixed_common.hpp"',
+           "",
+           "namespace sh {",
+           "namespace fixed {",
+           ""]
+    for p, (y0, y1) in enumerate(parts):
+        body = Body(k, rows, y0, y1).emit()
+        nr = y1 - y0
+        out.append(f"template <class Src>")
+        out.append(f"__device__ __forceinline__ void run_{name}_p{p}(const Src &src, const Sink &sink) {{")
+        out.append(f"    uint32_t acc[{nr}][8];")
+        # opaque zeros: a constant 0 would be folded into the first step, whose pinned results
+        # then need register copies of shared table entries (AGPR spills at k=200).
+        out.append(f"    for (int y = 0; y < {nr}; ++y) for (int b = 0; b < 8; ++b) ZERO(acc[y][b]);")
+        out.append(body)
+        out.append("    __builtin_amdgcn_sched_barrier(0);")
+        out.append(f"    // epilogue: (decode) + received recovery row, then store rows {y0}..{y1 - 1}")
+        for yi in range(nr):
+            out.append("    __builtin_amdgcn_sched_barrier(0);")
+            out.append(f"    src.add_row({y0 + yi}, acc[{yi}]);")
+            for b in range(8):
+                out.append(f"    sink.store({y0 + yi}, {b}, acc[{yi}][{b}]);")
+        out.append("}")
+        out.append("")
+    out.append(f"template <class Src>")
+    out.append(f"__device__ __forceinline__ void run_{name}(int part, const Src &src, const Sink &sink) {{")
+    for p in range(len(parts)):
+        kw = "if" if p == 0 else "else if"
+        out.append(f"    {kw} (part == {p}) run_{name}_p{p}(src, sink);")
+    out.append("}")
+    out.append("}  // namespace fixed")
+    out.append("}  // namespace sh")
+    out.append(f"FIXED_KERNELS({name}, {k}, {m}, {len(parts)})")
+    os.makedirs(OUTDIR, exist_ok=True)
+    path = os.path.join(OUTDIR, f"fixed_{name}.hip")
+    with open(path, "w") as f:
+        f.write("\n".join(out) + "\n")
+    return path
+
+
+def main():
+    cfgs = CONFIGS
+    if len(sys.argv) > 1:
+        cfgs = [tuple(map(int, a.split(","))) for a in sys.argv[1:]]
+    paths = [gen_config(k, m) for (k, m) in cfgs]
+    # registry of generated shapes
+    reg = ["// GENERATED by tools/gen_fixed_kernels.py -- list of compile-time-scheduled (k, m).",
+           "#pragma once", "#define SH_FIXED_CONFIGS(X) \\"]
+    reg += [f"    X({k}, {m}) \\" for (k, m) in CONFIGS]
+    reg.append("")
+    with open(os.path.join(OUTDIR, "fixed_configs.h"), "w") as f:
+        f.write("\n".join(reg) + "\n")
+    for p in paths:
+        print("wrote", os.path.relpath(p, ROOT))
+
+
+if __name__ == "__main__":
+    main()
