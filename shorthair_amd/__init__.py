@@ -18,7 +18,8 @@ __all__ = ["lib", "Block", "CAUCHY_256_VERSION", "cauchy_256_init", "cauchy_256_
            "EXPORTED_SYMBOLS"]
 
 CAUCHY_256_VERSION = 2
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcauchy256.so")
+LIB_PATH = os.environ.get("SH_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                         "libcauchy256.so")
 
 # Every symbol declared in include/cauchy_256.h and include/cauchy_256_batch.h.
 EXPORTED_SYMBOLS = [

@@ -11,11 +11,23 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-LIB = os.path.join(HERE, "libcauchy256.so")
+LIB = os.path.join(HERE, os.environ.get("SH_LIB_NAME", "libcauchy256.so"))
 SOURCES = ["kernels.hip", "fixed_dispatch.cpp", "cauchy_256_host.cpp"]
-GEN_DIR = os.path.join(CSRC, "gen")
+GEN_DIR = os.path.join(CSRC, os.environ.get("SH_GEN_DIR", "gen"))
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SH_OFFLOAD_ARCH", "gfx950")
+
+
+def generate():
+    """Emit csrc/gen/ (compile-time-scheduled kernels) from tools/gen_fixed_kernels.py."""
+    import importlib.util
+    path = os.path.join(HERE, "..", "tools", "gen_fixed_kernels.py")
+    spec = importlib.util.spec_from_file_location("gen_fixed_kernels", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    os.makedirs(GEN_DIR, exist_ok=True)
+    mod.OUTDIR = GEN_DIR
+    mod.main([])
 
 
 def _gen_sources():
@@ -33,7 +45,7 @@ def _stale():
 
 
 FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result"]
-OBJ_DIR = os.path.join(HERE, "build_obj")
+OBJ_DIR = os.path.join(HERE, os.environ.get("SH_OBJ_DIR", "build_obj"))
 
 
 def _compile(src, verbose):
@@ -42,7 +54,7 @@ def _compile(src, verbose):
             os.path.getmtime(src), os.path.getmtime(os.path.join(CSRC, "fixed_common.hpp")),
             os.path.getmtime(os.path.join(CSRC, "kernels.hpp"))):
         return obj, None
-    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+    cmd = [HIPCC] + FLAGS + [f"-I{GEN_DIR}", "-c", src, "-o", obj]
     if verbose:
         print(" ".join(cmd), flush=True)
     return obj, subprocess.Popen(cmd)
@@ -51,6 +63,12 @@ def _compile(src, verbose):
 def build(force=False, verbose=True, jobs=None):
     """Compile every source to build_obj/ (generated kernels in parallel: each is a large
     straight-line function, ~1-2 min for k=200) and link libcauchy256.so."""
+    gen_script = os.path.join(HERE, "..", "tools", "gen_fixed_kernels.py")
+    gen_inputs = max(os.path.getmtime(gen_script),
+                     os.path.getmtime(os.path.join(CSRC, "cauchy_tables_data.h")))
+    if (force or not os.path.isdir(GEN_DIR) or not _gen_sources()
+            or min(os.path.getmtime(f) for f in _gen_sources()) < gen_inputs):
+        generate()
     if not force and not _stale():
         return LIB
     os.makedirs(OBJ_DIR, exist_ok=True)

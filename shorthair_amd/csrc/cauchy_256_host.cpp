@@ -81,7 +81,8 @@ struct Context {
     uint8_t *d_exp = nullptr;         // 512
     uint16_t *d_log = nullptr;        // 256
     // (k, m) -> device generator: [m][round4(k)] coefficients (row 0 = ones) for encode,
-    // followed by the raw (m-1) x k rows 1..m-1 for decode setup.
+    // followed by the raw (m-1) x k rows 1..m-1 and the Cauchy parameters X'[k], Y'[m] for
+    // decode setup.
     std::map<std::pair<int, int>, uint8_t *> gens;
     DevBuf ws;                        // decode workspace
     // single-group staging, guarded by stage_mu for the whole call
@@ -134,10 +135,16 @@ uint8_t *generator(Context &c, int k, int m) {
     auto it = c.gens.find({k, m});
     if (it != c.gens.end()) return it->second;
     const std::vector<uint8_t> G = sh::generator_matrix(k, m);
+    std::vector<uint8_t> xp, yp;
+    sh::cauchy_params(k, m, xp, yp);
     const int ld = round4(k);
-    std::vector<uint8_t> host(static_cast<size_t>(m) * ld + static_cast<size_t>(m - 1) * k, 0);
+    const size_t raw = static_cast<size_t>(m) * ld;
+    const size_t par = raw + static_cast<size_t>(m - 1) * k;
+    std::vector<uint8_t> host(par + k + m, 0);
     for (int y = 0; y < m; ++y) std::memcpy(&host[static_cast<size_t>(y) * ld], &G[static_cast<size_t>(y) * k], k);
-    std::memcpy(&host[static_cast<size_t>(m) * ld], &G[k], static_cast<size_t>(m - 1) * k);
+    std::memcpy(&host[raw], &G[k], static_cast<size_t>(m - 1) * k);
+    std::memcpy(&host[par], xp.data(), k);
+    std::memcpy(&host[par + k], yp.data(), m);
     uint8_t *d = nullptr;
     if (hipMalloc(&d, host.size()) != hipSuccess) return nullptr;
     if (hipMemcpy(d, host.data(), host.size(), hipMemcpyHostToDevice) != hipSuccess) return nullptr;
@@ -268,6 +275,8 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
     sa.rows = d_rows;
     sa.rows_gstride = k;
     sa.gen = gen + static_cast<size_t>(m) * round4(k);
+    sa.xp = sa.gen + static_cast<size_t>(m - 1) * k;
+    sa.yp = sa.xp + k;
     sa.gf_exp = c.d_exp;
     sa.gf_log = c.d_log;
     sa.emax = w.emax;

@@ -110,4 +110,19 @@ inline std::vector<uint8_t> generator_matrix(int k, int m) {
     return G;
 }
 
+// Cauchy parameters of the m >= 7 generator: C[y][x] = X'_x / (X'_x + Y'_y) with X'_0 = 1,
+// X'_x = X[x-1] and Y'_0 = 0, Y'_y = Y[y-1] (same tables as generator_matrix()). Empty for m < 7.
+inline void cauchy_params(int k, int m, std::vector<uint8_t> &xp, std::vector<uint8_t> &yp) {
+    xp.assign(static_cast<size_t>(k), 0);
+    yp.assign(static_cast<size_t>(m), 0);
+    if (m < 7) return;
+    const GeneratorTables &t = gen_tables();
+    const int n = m - 7;
+    const uint8_t *X = t.X.data() + n * 249 - n * (n + 1) / 2;
+    xp[0] = 1;
+    for (int x = 1; x < k; ++x) xp[x] = X[x - 1];
+    yp[0] = 0;
+    for (int y = 1; y < m; ++y) yp[y] = t.Y[y - 1];
+}
+
 }  // namespace sh

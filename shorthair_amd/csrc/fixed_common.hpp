@@ -207,7 +207,7 @@ struct Sink {
 
 // Kernel + launcher for one generated (k, m). LDS: decode position tables of the groups a
 // workgroup touches ([groups_per_wg][round4(K) + round4(M)] bytes).
-#define FIXED_KERNELS(NAME, K, M, P)                                                              \
+#define FIXED_KERNELS(NAME, K, M, P, RPP)                                                            \
     namespace sh {                                                                                \
     namespace fixed {                                                                             \
     template <bool DEC>                                                                           \

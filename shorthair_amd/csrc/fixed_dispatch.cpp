@@ -1,7 +1,7 @@
 // Dispatch to the compile-time-scheduled kernels generated for specific (k, m).
 #include <hip/hip_runtime.h>
 
-#include "gen/fixed_configs.h"
+#include "fixed_configs.h"  // from the generated-kernel directory (-I, see build.py)
 #include "kernels.hpp"
 
 namespace sh {

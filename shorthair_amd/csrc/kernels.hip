@@ -216,28 +216,40 @@ __global__ __launch_bounds__(256) void copy_first(const uint8_t *in, long long i
 }
 
 // ---------------------------------------------------------------------------------------------
-// Decode setup, one 64-lane workgroup per group (reference sort_blocks + generate_bitmatrix,
-// cauchy_256.cpp:522-554, :691-774, restated in GF(256)):
+// Decode setup, one 64-lane workgroup (one wave) per group. Restates the reference's
+// sort_blocks + generate_bitmatrix (cauchy_256.cpp:522-554, :691-774) in GF(256):
 //   * originals (row < k) / recovery blocks (row >= k) in array order; erasures = missing
 //     original rows ascending; e = number of recovery blocks (0 -> nothing to do);
-//   * stage-A coefficients  A[i][j]: residual_i = R_i + sum_{orig j} C[r_i][row_j] * d_j
-//     (= 1 on block rec[i] itself, 0 on the other recovery blocks);
-//   * stage-B coefficients  S^-1 with S[i][l] = C[r_i][erasure_l], by Gauss-Jordan in LDS.
-// The recovered erasure l is then sum_i M(S^-1[l][i]) residual_i; it goes to the l-th recovery
-// block in array order, whose row becomes erasure_l (reference row contract, :548-553, :770).
+//   * S[i][j] = C[r_i][E_j] over received recovery rows r_i and erased columns E_j, and
+//     x_{E_j} = S^-1 applied to the residuals. The recovered erasure j goes to the j-th recovery
+//     block in array order, whose row becomes E_j (reference row contract, :548-553, :770).
+// S^-1: for m >= 7 the generator is a scaled Cauchy matrix, C[y][x] = X'_x / (X'_x + Y'_y)
+// (X'_0 = 1, Y'_0 = 0 gives the all-ones row 0; cauchy_256.cpp:453-477), so
+//   S^-1[j][i] = a_j b_i / (x_j (x_j + y_i)),  a_j = prod_k (x_j+y_k) / prod_{k!=j} (x_j+x_k),
+//                                              b_i = prod_k (x_k+y_i) / prod_{k!=i} (y_i+y_k)
+// with x_j = X'_{E_j}, y_i = Y'_{r_i}: O(e^2) log-domain table lookups, no elimination. The
+// static "improved" tables for m = 2..6 have no such structure; there e <= 5 and a small
+// Gauss-Jordan in LDS does it.
 // ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int mod255(int v) {
+    v %= 255;
+    return v < 0 ? v + 255 : v;
+}
+
 __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
     const int g = blockIdx.x;
     const int lane = threadIdx.x;
-    const int k = a.k;
+    const int k = a.k, m = a.m;
     __shared__ uint8_t s_exp[512];
     __shared__ uint8_t s_log[256];
     __shared__ uint8_t s_rows[256];
     __shared__ uint8_t s_present[256];
     __shared__ uint8_t s_rec[256];      // array index of the i-th recovery block
     __shared__ uint8_t s_rrow[256];     // its generator row r_i = row - k
-    __shared__ uint8_t s_era[256];      // i-th erased original row
-    __shared__ uint8_t s_mat[128 * 256];  // [S | I] rows of width 2e (e <= 128)
+    __shared__ uint8_t s_era[256];      // j-th erased original row E_j
+    __shared__ uint8_t s_x[256], s_y[256];
+    __shared__ int s_la[256], s_lb[256], s_lx[256];
+    __shared__ uint8_t s_gj[6 * 12];    // [S | I] for the m <= 6 Gauss-Jordan
     __shared__ int s_piv;
 
     for (int i = lane; i < 512; i += 64) s_exp[i] = a.gf_exp[i];
@@ -252,7 +264,7 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
         if (s_rows[j] < k) s_present[s_rows[j]] = 1;
     __syncthreads();
 
-    // Ordered compaction with wave ballots (64 lanes = one wave).
+    // Ordered compaction with wave ballots (the workgroup is one wave).
     int nrec = 0;
     for (int base = 0; base < k; base += 64) {
         const int j = base + lane;
@@ -272,114 +284,142 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
         const unsigned long long mask = __ballot(miss);
         if (miss) {
             const int pos = nera + __popcll(mask & ((1ull << lane) - 1ull));
-            if (pos < 256) s_era[pos] = static_cast<uint8_t>(x);
+            s_era[pos] = static_cast<uint8_t>(x);
         }
         nera += __popcll(mask);
     }
     __syncthreads();
     const int e = nrec;
     if (lane == 0) a.e_out[g] = e;
-    if (e == 0) return;
-    // (A caller that hands more recovery blocks than erasures breaks the reference's
-    //  precondition; we clamp like the reference's erasure scan, cauchy_256.cpp:548.)
-    const int emax = a.emax;
-
-    uint8_t *rec_idx = a.rec_idx + static_cast<long long>(g) * emax;
-    uint8_t *era = a.erasures + static_cast<long long>(g) * emax;
-    for (int i = lane; i < e; i += 64) {
-        rec_idx[i] = s_rec[i];
-        era[i] = (i < nera) ? s_era[i] : 0;
-    }
-
-    auto gmul = [&](uint32_t x, uint32_t y) -> uint32_t {
-        return (x && y) ? s_exp[s_log[x] + s_log[y]] : 0u;
-    };
-    auto C = [&](int r, int x) -> uint32_t {
-        return r == 0 ? 1u : a.gen[static_cast<long long>(r - 1) * k + x];
-    };
-
     const bool fixed_mode = (a.coefA == nullptr);
     if (fixed_mode) {
-        const int KP = (k + 3) & ~3, MP = (a.m + 3) & ~3;
+        const int KP = (k + 3) & ~3, MP = (m + 3) & ~3;
         uint8_t *pos = a.pos + static_cast<long long>(g) * KP;
         uint8_t *rpos = a.rpos + static_cast<long long>(g) * MP;
         for (int x = lane; x < KP; x += 64) pos[x] = 0xFF;
         for (int y = lane; y < MP; y += 64) rpos[y] = 0xFF;
-        __syncthreads();
-        for (int j = lane; j < k; j += 64) {
+        for (int j = lane; j < k; j += 64) {  // same wave, issued after the fills: ordered
             const int row = s_rows[j];
             if (row < k) pos[row] = static_cast<uint8_t>(j);
-            else if (row - k < a.m) rpos[row - k] = static_cast<uint8_t>(j);
+            else if (row - k < m) rpos[row - k] = static_cast<uint8_t>(j);
         }
     }
-    // Stage-A coefficients, row-major [i][j], leading dimension ldA.
-    uint8_t *A = fixed_mode ? nullptr : a.coefA + static_cast<long long>(g) * a.coefA_gstride;
-    for (int i = 0; i < e && !fixed_mode; ++i) {
-        const int r = s_rrow[i];
-        for (int j = lane; j < a.ldA; j += 64) {
-            uint32_t c = 0;
-            if (j < k) {
-                const int row = s_rows[j];
-                c = row < k ? C(r, row) : (j == s_rec[i] ? 1u : 0u);
+    if (e == 0) return;
+    if (nera < e) {  // more recovery blocks than erasures: outside the reference's contract
+        if (lane == 0) a.e_out[g] = -1;
+        return;
+    }
+    const int emax = a.emax;
+    uint8_t *rec_idx = a.rec_idx + static_cast<long long>(g) * emax;
+    uint8_t *era = a.erasures + static_cast<long long>(g) * emax;
+    for (int i = lane; i < e; i += 64) {
+        rec_idx[i] = s_rec[i];
+        era[i] = s_era[i];
+    }
+    auto C = [&](int r, int x) -> uint32_t {
+        return r == 0 ? 1u : a.gen[static_cast<long long>(r - 1) * k + x];
+    };
+
+    // Stage-A coefficients (generic path only), row-major [i][j], leading dimension ldA.
+    if (!fixed_mode) {
+        uint8_t *A = a.coefA + static_cast<long long>(g) * a.coefA_gstride;
+        for (int i = 0; i < e; ++i) {
+            const int r = s_rrow[i];
+            for (int j = lane; j < a.ldA; j += 64) {
+                uint32_t c = 0;
+                if (j < k) {
+                    const int row = s_rows[j];
+                    c = row < k ? C(r, row) : (j == s_rec[i] ? 1u : 0u);
+                }
+                A[static_cast<long long>(i) * a.ldA + j] = static_cast<uint8_t>(c);
             }
-            A[static_cast<long long>(i) * a.ldA + j] = static_cast<uint8_t>(c);
         }
     }
 
-    // Gauss-Jordan on [S | I] over GF(256).
+    // Stage-B coefficients: coefB[j][col] = S^-1[j][i], col = r_i (fixed path, rows of the
+    // residual) or i (generic path); zero elsewhere.
+    uint8_t *Bc = a.coefB + static_cast<long long>(g) * a.coefB_gstride;
+    for (int j = 0; j < e; ++j)
+        for (int c = lane; c < a.ldB; c += 64) Bc[static_cast<long long>(j) * a.ldB + c] = 0;
+    auto put = [&](int j, int i, uint32_t v) {
+        const int col = fixed_mode ? s_rrow[i] : i;
+        Bc[static_cast<long long>(j) * a.ldB + col] = static_cast<uint8_t>(v);
+    };
+    if (m >= 7) {
+        for (int t = lane; t < e; t += 64) {
+            s_x[t] = a.xp[s_era[t]];
+            s_y[t] = a.yp[s_rrow[t]];
+        }
+        __syncthreads();
+        for (int t = lane; t < e; t += 64) {
+            const int xt = s_x[t], yt = s_y[t];
+            int la = 0, lb = 0;
+            for (int q = 0; q < e; ++q) {
+                la += s_log[xt ^ s_y[q]];
+                lb += s_log[s_x[q] ^ yt];
+                if (q != t) {
+                    la -= s_log[xt ^ s_x[q]];
+                    lb -= s_log[yt ^ s_y[q]];
+                }
+            }
+            s_la[t] = la;
+            s_lb[t] = lb;
+            s_lx[t] = s_log[xt];
+        }
+        __syncthreads();
+        // (writes after the zero fill above: same wave, program order)
+        for (int t = lane; t < e * e; t += 64) {
+            const int j = t / e, i = t - j * e;
+            const int l = s_la[j] + s_lb[i] - s_lx[j] - s_log[s_x[j] ^ s_y[i]];
+            put(j, i, s_exp[mod255(l)]);
+        }
+        return;
+    }
+    // m <= 6: Gauss-Jordan on [S | I] (e <= 5).
     const int w = 2 * e;
-    for (int i = 0; i < e; ++i)
-        for (int c = lane; c < w; c += 64)
-            s_mat[i * w + c] = static_cast<uint8_t>(c < e ? C(s_rrow[i], s_era[c]) : (c - e == i ? 1 : 0));
+    for (int t = lane; t < e * w; t += 64) {
+        const int i = t / w, c = t - i * w;
+        s_gj[i * w + c] = static_cast<uint8_t>(c < e ? C(s_rrow[i], s_era[c]) : (c - e == i ? 1 : 0));
+    }
     __syncthreads();
+    auto gmul = [&](uint32_t x, uint32_t y) -> uint32_t {
+        return (x && y) ? s_exp[s_log[x] + s_log[y]] : 0u;
+    };
     for (int col = 0; col < e; ++col) {
         if (lane == 0) {
             int p = -1;
             for (int r = col; r < e; ++r)
-                if (s_mat[r * w + col]) { p = r; break; }
+                if (s_gj[r * w + col]) { p = r; break; }
             s_piv = p;
         }
         __syncthreads();
         const int p = s_piv;
-        if (p < 0) {  // singular: impossible for a Cauchy submatrix; flag and stop
+        if (p < 0) {  // singular: impossible for an MDS submatrix
             if (lane == 0) a.e_out[g] = -1;
             return;
         }
-        if (p != col)
-            for (int c = lane; c < w; c += 64) {
-                const uint8_t t = s_mat[p * w + c];
-                s_mat[p * w + c] = s_mat[col * w + c];
-                s_mat[col * w + c] = t;
+        if (lane < w && p != col) {
+            const uint8_t t = s_gj[p * w + lane];
+            s_gj[p * w + lane] = s_gj[col * w + lane];
+            s_gj[col * w + lane] = t;
+        }
+        __syncthreads();
+        const uint32_t pinv = s_exp[255 - s_log[s_gj[col * w + col]]];
+        if (lane < w) s_gj[col * w + lane] = static_cast<uint8_t>(gmul(s_gj[col * w + lane], pinv));
+        __syncthreads();
+        if (lane < w)
+            for (int r = 0; r < e; ++r) {
+                if (r == col) continue;
+                const uint32_t f = s_gj[r * w + col];
+                if (f && lane != col) s_gj[r * w + lane] ^= static_cast<uint8_t>(gmul(f, s_gj[col * w + lane]));
             }
         __syncthreads();
-        const uint32_t pv = s_mat[col * w + col];
-        const uint32_t pinv = s_exp[255 - s_log[pv]];
-        for (int c = lane; c < w; c += 64) s_mat[col * w + c] = static_cast<uint8_t>(gmul(s_mat[col * w + c], pinv));
-        __syncthreads();
-        for (int idx = lane; idx < e * w; idx += 64) {
-            const int r = idx / w, c = idx - r * w;
-            if (r == col) continue;
-            const uint32_t f = s_mat[r * w + col];
-            if (f && c != col) s_mat[r * w + c] ^= static_cast<uint8_t>(gmul(f, s_mat[col * w + c]));
-        }
-        __syncthreads();
-        for (int r = lane; r < e; r += 64)
-            if (r != col) s_mat[r * w + col] = 0;
+        if (lane < e && lane != col) s_gj[lane * w + col] = 0;
         __syncthreads();
     }
-    uint8_t *Bc = a.coefB + static_cast<long long>(g) * a.coefB_gstride;
-    if (fixed_mode) {
-        // coefB[l][y] = S^-1[l][i] where r_i = y; zero for rows that were not received
-        for (int l = 0; l < e; ++l) {
-            for (int y = lane; y < a.ldB; y += 64) Bc[static_cast<long long>(l) * a.ldB + y] = 0;
-            __syncthreads();
-            for (int i = lane; i < e; i += 64) Bc[static_cast<long long>(l) * a.ldB + s_rrow[i]] = s_mat[l * w + e + i];
-            __syncthreads();
-        }
-    } else {
-        for (int l = 0; l < e; ++l)
-            for (int i = lane; i < a.ldB; i += 64)
-                Bc[static_cast<long long>(l) * a.ldB + i] = static_cast<uint8_t>(i < e ? s_mat[l * w + e + i] : 0);
+    for (int t = lane; t < e * e; t += 64) {
+        const int j = t / e, i = t - j * e;
+        put(j, i, s_gj[j * w + e + i]);
     }
 }
 

@@ -48,6 +48,8 @@ struct DecodeSetupArgs {
     const uint8_t *rows;    // [G][rows_gstride] block rows as handed in
     long long rows_gstride;
     const uint8_t *gen;     // (m-1) x k generator rows 1..m-1
+    const uint8_t *xp;      // m >= 7: X'[x], x < k  (generator column parameters, X'_0 = 1)
+    const uint8_t *yp;      // m >= 7: Y'[y], y < m  (generator row parameters, Y'_0 = 0)
     const uint8_t *gf_exp;  // 512
     const uint16_t *gf_log; // 256
     int emax;

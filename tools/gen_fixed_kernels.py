@@ -18,17 +18,20 @@ Rows are split into parts of <= 16 rows (128 accumulator VGPRs); the waves of on
 run the parts of the same columns, so the second part's loads hit L1/L2.
 
 Usage: python tools/gen_fixed_kernels.py            (all configs in CONFIGS)
+Run by shorthair_amd/build.py before compiling; the generated files are not committed.
 """
 import os
 import sys
 
 ROOT = os.path.normpath(os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
-sys.path.insert(0, ROOT)
 OUTDIR = os.path.join(ROOT, "shorthair_amd", "csrc", "gen")
 
 # (k, m): BASELINE.json configs -- headline (200,32), C2 (64,16), C4 sweep (28,4),(112,16),(224,32)
 CONFIGS = [(200, 32), (64, 16), (28, 4), (112, 16), (224, 32)]
-ROWS_PER_PART = 16
+if os.environ.get("SH_CONFIGS"):  # experiments: e.g. SH_CONFIGS="200,32;64,16"
+    CONFIGS = [tuple(map(int, c.split(","))) for c in os.environ["SH_CONFIGS"].split(";")]
+ROWS_PER_PART = int(os.environ.get("SH_ROWS_PER_PART", "16"))
+PREFETCH = int(os.environ.get("SH_PREFETCH", "2"))
 
 
 def gf_tables():
@@ -51,13 +54,37 @@ def gmul(a, b):
     return 0 if a == 0 or b == 0 else EXP[LOG[a] + LOG[b]]
 
 
+def _tables():
+    """Decode the generator-table data the product ships (csrc/cauchy_tables_data.h)."""
+    import re
+    text = open(os.path.join(ROOT, "shorthair_amd", "csrc", "cauchy_tables_data.h")).read()
+    out = {}
+    for m in re.finditer(r"static const char SH_TABLE_(\w+)_HEX\[\] =\s*((?:\s*\"[0-9a-f]*\")+);", text):
+        out[m.group(1)] = bytes.fromhex("".join(re.findall(r'"([0-9a-f]*)"', m.group(2))))
+    return out
+
+
 def generator(k, m):
-    """Full m x k generator (row 0 = ones) from the oracle's restatement of cauchy_matrix()."""
-    from oracle import pyoracle as po
+    """Full m x k generator (row 0 = ones), restating the reference's cauchy_matrix()
+    (cauchy_256.cpp:423-481) exactly as csrc/cauchy_math.hpp does."""
     rows = [[1] * k]
-    if m >= 2:
-        mat = po.cauchy_matrix(k, m)
-        rows += [list(map(int, mat[y])) for y in range(m - 1)]
+    if m < 2:
+        return rows
+    t = _tables()
+    if m <= 6:
+        stat, stride = t[str(m)], 256 - m
+        rows += [list(stat[(y - 1) * stride:(y - 1) * stride + k]) for y in range(1, m)]
+        return rows
+    n = m - 7
+    X = t["X"][n * 249 - n * (n + 1) // 2:]
+    Y = t["Y"]
+    inv = [0] + [EXP[(255 - LOG[a]) % 255] for a in range(1, 256)]
+
+    def div(a, b):
+        return 0 if a == 0 or b == 0 else EXP[LOG[a] + 255 - LOG[b]]
+    for y in range(1, m):
+        G = Y[y - 1]
+        rows.append([inv[1 ^ G]] + [div(X[x - 1], X[x - 1] ^ G) for x in range(1, k)])
     return rows
 
 
@@ -96,7 +123,7 @@ class Body:
         have.add(name)
         return name
 
-    def emit(self, pf=2):
+    def emit(self, pf=PREFETCH):
         """Inputs are prefetched `pf` steps ahead into a ring of register sets (raw words; the
         only per-step fix-up is Src::fix7 for the buffer-end tail lane)."""
         L = self.lines
@@ -179,7 +206,7 @@ def gen_config(k, m):
     out.append("}")
     out.append("}  // namespace fixed")
     out.append("}  // namespace sh")
-    out.append(f"FIXED_KERNELS({name}, {k}, {m}, {len(parts)})")
+    out.append(f"FIXED_KERNELS({name}, {k}, {m}, {len(parts)}, {ROWS_PER_PART})")
     os.makedirs(OUTDIR, exist_ok=True)
     path = os.path.join(OUTDIR, f"fixed_{name}.hip")
     with open(path, "w") as f:
@@ -187,10 +214,10 @@ def gen_config(k, m):
     return path
 
 
-def main():
+def main(argv=()):
     cfgs = CONFIGS
-    if len(sys.argv) > 1:
-        cfgs = [tuple(map(int, a.split(","))) for a in sys.argv[1:]]
+    if argv:
+        cfgs = [tuple(map(int, a.split(","))) for a in argv]
     paths = [gen_config(k, m) for (k, m) in cfgs]
     # registry of generated shapes
     reg = ["// GENERATED by tools/gen_fixed_kernels.py -- list of compile-time-scheduled (k, m).",
@@ -204,4 +231,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])
