@@ -12,7 +12,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, os.environ.get("SH_LIB_NAME", "libcauchy256.so"))
-SOURCES = ["kernels.hip", "fixed_dispatch.cpp", "cauchy_256_host.cpp"]
+SOURCES = ["kernels.hip", "stageb.hip", "fixed_dispatch.cpp", "cauchy_256_host.cpp"]
 GEN_DIR = os.path.join(CSRC, os.environ.get("SH_GEN_DIR", "gen"))
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SH_OFFLOAD_ARCH", "gfx950")

@@ -240,10 +240,10 @@ size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool n
     w.fixed = sh::has_fixed(k, m, B);
     w.emax = std::min(k, m);
     w.ldA = w.fixed ? 0 : round4(k);
-    w.ldB = w.fixed ? round4(m) : round4(w.emax);
+    w.ldB = (w.emax + 7) & ~7;  // stage-B coefficients [n_in][ldB] (transposed, 8-byte rows)
     w.nres = w.fixed ? m : w.emax;
     w.coefA_gs = static_cast<long long>(w.emax) * w.ldA;
-    w.coefB_gs = static_cast<long long>(w.emax) * w.ldB;
+    w.coefB_gs = static_cast<long long>(w.nres) * w.ldB;
     size_t off = 0;
     auto take = [&](size_t bytes) {
         uint8_t *p = base ? base + off : nullptr;
@@ -258,9 +258,26 @@ size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool n
     w.coefB = take(G * w.coefB_gs);
     w.pos = w.fixed ? take(G * round4(k)) : nullptr;
     w.rpos = w.fixed ? take(G * round4(m)) : nullptr;
-    w.residual = take(G * w.nres * static_cast<size_t>(B));
+    w.residual = take(G * w.nres * static_cast<size_t>(B) + 256);  // + slack: word over-read
     w.recovered = need_recovered ? take(G * w.emax * static_cast<size_t>(B)) : nullptr;
     return off;
+}
+
+hipError_t launch_stage_b(Context &, const DecodeWS &w, int n_in, int B, int groups, uint8_t *dst,
+                          hipStream_t s) {
+    sh::StageBArgs b{};
+    b.in = w.residual;
+    b.in_gstride = static_cast<long long>(n_in) * B;
+    b.n_in = n_in;
+    b.out = dst;
+    b.out_gstride = static_cast<long long>(w.emax) * B;
+    b.e = w.e;
+    b.coefT = w.coefB;
+    b.coefT_gstride = w.coefB_gs;
+    b.ldT = w.ldB;
+    b.groups = groups;
+    b.geo = sh::make_geometry(B);
+    return sh::launch_stageb(b, w.emax, s);
 }
 
 // Common decode core (m >= 2, valid params): writes recovered blocks densely into `dst`
@@ -299,24 +316,8 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
         //   residual_y = R_y + sum_{received x} M(C[y][x]) d_x
         SH_CHECK(launch_fixed_chunked(k, m, B, groups, d_blocks, static_cast<long long>(k) * B,
                                       w.residual, static_cast<long long>(m) * B, w.pos, w.rpos, true, s));
-        // Stage B: recovered_l = sum_y M(coefB[l][y]) residual_y  (coefB = S^-1 on received rows)
-        sh::ApplyArgs b{};
-        b.in = w.residual;
-        b.in_gstride = static_cast<long long>(m) * B;
-        b.in_bstride = B;
-        b.n_in = m;
-        b.out = dst;
-        b.out_gstride = static_cast<long long>(w.emax) * B;
-        b.out_bstride = B;
-        b.n_out = w.emax;
-        b.n_out_g = w.e;
-        b.coef = w.coefB;
-        b.coef_gstride = w.coefB_gs;
-        b.coef_ld = w.ldB;
-        b.rowbytes = c.d_rowbytes;
-        b.groups = groups;
-        b.geo = geo;
-        SH_CHECK(sh::launch_apply(b, true, s));
+        // Stage B: recovered_j = sum_y M(S^-1[j][i(y)]) residual_y over the received rows y
+        SH_CHECK(launch_stage_b(c, w, m, B, groups, dst, s));
         return 0;
     }
     // Stage A: residual_i = R_i + sum_{orig j} M(C[r_i][row_j]) d_j  (per-group coefficients)
@@ -337,21 +338,11 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
     a.groups = groups;
     a.geo = geo;
     SH_CHECK(sh::launch_apply(a, true, s));
-    // Stage B: recovered_l = sum_i M(S^-1[l][i]) residual_i
-    sh::ApplyArgs b = a;
-    b.in = w.residual;
-    b.in_gstride = static_cast<long long>(w.emax) * B;
-    b.n_in = w.emax;
-    b.out = dst;
-    b.coef = w.coefB;
-    b.coef_gstride = w.coefB_gs;
-    b.coef_ld = w.ldB;
-    SH_CHECK(sh::launch_apply(b, true, s));
+    // Stage B: recovered_j = sum_i M(S^-1[j][i]) residual_i
+    SH_CHECK(launch_stage_b(c, w, w.emax, B, groups, dst, s));
     return 0;
 }
 
-// Invalid parameters: the reference returns -1 only when a group actually has something to
-// recover (cauchy_256.cpp:1266-1273); find out on the host (rare path, synchronous).
 int invalid_decode_status(int k, int groups, const uint8_t *d_rows, hipStream_t s) {
     std::vector<uint8_t> rows(static_cast<size_t>(groups) * k);
     SH_CHECK(hipMemcpyAsync(rows.data(), d_rows, rows.size(), hipMemcpyDeviceToHost, s));

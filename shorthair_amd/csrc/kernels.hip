@@ -336,14 +336,14 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
         }
     }
 
-    // Stage-B coefficients: coefB[j][col] = S^-1[j][i], col = r_i (fixed path, rows of the
-    // residual) or i (generic path); zero elsewhere.
+    // Stage-B coefficients, transposed for the snippet kernel: coefB[col][j] = S^-1[j][i] with
+    // col = r_i (fixed path: rows of the residual) or i (generic path); zero elsewhere.
     uint8_t *Bc = a.coefB + static_cast<long long>(g) * a.coefB_gstride;
-    for (int j = 0; j < e; ++j)
-        for (int c = lane; c < a.ldB; c += 64) Bc[static_cast<long long>(j) * a.ldB + c] = 0;
+    const int ncol = fixed_mode ? m : emax;
+    for (int t = lane; t < ncol * a.ldB; t += 64) Bc[t] = 0;
     auto put = [&](int j, int i, uint32_t v) {
         const int col = fixed_mode ? s_rrow[i] : i;
-        Bc[static_cast<long long>(j) * a.ldB + col] = static_cast<uint8_t>(v);
+        Bc[static_cast<long long>(col) * a.ldB + j] = static_cast<uint8_t>(v);
     };
     if (m >= 7) {
         for (int t = lane; t < e; t += 64) {

@@ -59,9 +59,9 @@ struct DecodeSetupArgs {
     uint8_t *coefA;         // [G][emax][ldA]
     long long coefA_gstride;
     int ldA;
-    uint8_t *coefB;         // [G][emax][ldB]
+    uint8_t *coefB;         // stage-B coefficients, TRANSPOSED: [G][n_in][ldB], entry [y][j]
     long long coefB_gstride;
-    int ldB;
+    int ldB;                // >= emax, multiple of 8
     // Fixed-kernel mode (coefA == nullptr): stage A runs the compile-time generator over all m
     // rows, so the setup emits position tables instead of stage-A coefficients, and stage B's
     // coefficients are indexed by generator row y (coefB[l][y], ldB >= m) rather than by i.
@@ -82,6 +82,22 @@ struct ScatterArgs {
     int emax;
     int B;
 };
+
+// Decode stage B (csrc/stageb.hip): out[g][j] = sum_y M(coefT[g][y][j]) in[g][y], j < e[g].
+struct StageBArgs {
+    const uint8_t *in;        // [G][n_in][B] residual rows (>= 4 readable slack bytes at the end)
+    long long in_gstride;
+    int n_in;
+    uint8_t *out;             // [G][emax][B]
+    long long out_gstride;
+    const int *e;             // [G] outputs per group
+    const uint8_t *coefT;     // [G][n_in][ldT], ldT % 8 == 0
+    long long coefT_gstride;
+    int ldT;
+    int groups;
+    Geometry geo;
+};
+hipError_t launch_stageb(const StageBArgs &a, int emax, hipStream_t stream);
 
 // Compile-time-scheduled kernels (csrc/gen/, tools/gen_fixed_kernels.py).
 struct FixedArgs {

@@ -1,0 +1,135 @@
+// Runtime-coefficient bitmatrix product through a table of compile-time snippets (decode stage B).
+//
+//   out[g][j] = sum_y M(coef[g][y][j]) * in[g][y]        (j < e_g outputs, y < n_in inputs)
+//
+// The coefficients (S^-1 of a group's erasure pattern) are only known at run time, so the
+// compile-time schedule of the encode kernels does not apply, and a register table indexed by a
+// runtime (wave-uniform) value costs 8.7x (hipcc's s_set_gpr_idx lowering). Here the
+// runtime choice is made ONCE per coefficient instead of once per table lookup: 256 snippets,
+// one per coefficient value c, each computing tmp[b] = T0[lo(c*2^b)] ^ T1[hi(c*2^b)] for b = 0..7
+// with compile-time register operands, are emitted inside the kernel (csrc/gen/snippets.h); the
+// kernel reaches snippet c with one s_swappc_b64 and returns with s_setpc_b64. The window tables
+// T0/T1 of the current input (the reference's win_encode tables, cauchy_256.cpp:1426-1445) and
+// tmp live in VGPRs pinned through explicit-register asm operands, so hipcc keeps its own values
+// out of them.
+//
+// One workgroup = one group x 64 word columns x 32 outputs (4 waves x 8 outputs). Group-uniform
+// coefficients require a wave to stay inside one group: at B = 1400 a group has 44 word columns.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.hpp"
+#include "snippets.h"
+
+namespace sh {
+
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ uint32_t ldw_b(const uint8_t *p) {
+    uint32_t w;
+    __builtin_memcpy(&w, p, 4);
+    return w;
+}
+
+// Call snippet at `target`: tmp = M(c) * (input whose window tables are t0/t1).
+#define SH_SNIP_CALL(target, t0, t1, tmp)                                                         \
+    asm volatile("s_swappc_b64 s[40:41], %[tg]"                                                  \
+                 : "={v[132:139]}"(tmp)                                                          \
+                 : [tg] "s"(target), "{v[100:115]}"(t0), "{v[116:131]}"(t1)                      \
+                 : "s40", "s41")
+
+static_assert(SH_SNIP_T0 == 100 && SH_SNIP_T1 == 116 && SH_SNIP_TMP == 132,
+              "snippet registers must match the call constraints");
+
+__global__ __launch_bounds__(256) void stageb_snip(StageBArgs a) {
+    SH_SNIPPET_TABLE(B);
+    const int ncc = (a.geo.nq + 63) / 64;  // 64-column chunks per group
+    const int g = blockIdx.x / ncc;
+    const int cc = blockIdx.x - g * ncc;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int j0 = (blockIdx.y * 4 + wave) * 8;
+    const int e = a.e[g];
+    if (j0 >= e) return;  // wave-uniform
+    const int q = cc * 64 + lane;
+    const Geometry geo = a.geo;
+    if (q >= geo.nq) return;  // idle lanes (e.g. 20 of 64 at B = 1400)
+
+    uint64_t base;
+    asm volatile(
+        "s_getpc_b64 s[42:43]\n"
+        "s_add_u32 s42, s42, sh_snip_baseB@rel32@lo+4\n"
+        "s_addc_u32 s43, s43, sh_snip_baseB@rel32@hi+12\n"
+        "s_mov_b64 %0, s[42:43]"
+        : "=s"(base)
+        :
+        : "s42", "s43", "scc");
+
+    const uint8_t *in = a.in + static_cast<long long>(g) * a.in_gstride + 4 * q;
+    const uint8_t *coef = a.coefT + static_cast<long long>(g) * a.coefT_gstride + j0;
+
+    uint32_t acc[8][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[j][b] = 0;
+
+    for (int y = 0; y < a.n_in; ++y) {
+        const uint64_t cw = *reinterpret_cast<const uint64_t *>(coef + static_cast<long long>(y) * a.ldT);
+        if (cw == 0) continue;  // wave-uniform: no output of this wave uses input y
+        const uint8_t *blk = in + static_cast<long long>(y) * geo.B;
+        uint32_t d[8];
+#pragma unroll
+        for (int s = 0; s < 8; ++s) d[s] = ldw_b(blk + s * geo.sub);
+        u32x16 t0, t1;
+        t0[0] = 0;
+        t1[0] = 0;
+        t0[1] = d[0]; t0[2] = d[1]; t0[4] = d[2]; t0[8] = d[3];
+        t1[1] = d[4]; t1[2] = d[5]; t1[4] = d[6]; t1[8] = d[7];
+        t0[3] = t0[1] ^ t0[2]; t0[5] = t0[1] ^ t0[4]; t0[6] = t0[2] ^ t0[4]; t0[7] = t0[3] ^ t0[4];
+        t0[9] = t0[1] ^ t0[8]; t0[10] = t0[2] ^ t0[8]; t0[11] = t0[3] ^ t0[8]; t0[12] = t0[4] ^ t0[8];
+        t0[13] = t0[5] ^ t0[8]; t0[14] = t0[6] ^ t0[8]; t0[15] = t0[7] ^ t0[8];
+        t1[3] = t1[1] ^ t1[2]; t1[5] = t1[1] ^ t1[4]; t1[6] = t1[2] ^ t1[4]; t1[7] = t1[3] ^ t1[4];
+        t1[9] = t1[1] ^ t1[8]; t1[10] = t1[2] ^ t1[8]; t1[11] = t1[3] ^ t1[8]; t1[12] = t1[4] ^ t1[8];
+        t1[13] = t1[5] ^ t1[8]; t1[14] = t1[6] ^ t1[8]; t1[15] = t1[7] ^ t1[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t c = static_cast<uint32_t>(cw >> (8 * j)) & 0xffu;
+            if (c == 0) continue;  // wave-uniform
+            u32x8 tmp;
+            SH_SNIP_CALL(base + (static_cast<uint64_t>(c) << 6), t0, t1, tmp);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) acc[j][b] ^= tmp[b];
+        }
+    }
+
+    // Store the rows this wave owns; a sub-block's short last word is stored byte-exact.
+    const bool last = (q == geo.nq - 1);
+    const int nbytes = last ? geo.tail : 4;
+    uint8_t *out = a.out + static_cast<long long>(g) * a.out_gstride + 4 * q;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (j0 + j >= e) break;
+        uint8_t *row = out + static_cast<long long>(j0 + j) * geo.B;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            uint8_t *p = row + b * geo.sub;
+            const uint32_t w = acc[j][b];
+            if (nbytes == 4) {
+                __builtin_memcpy(p, &w, 4);
+            } else {
+                for (int i = 0; i < nbytes; ++i) p[i] = static_cast<uint8_t>(w >> (8 * i));
+            }
+        }
+    }
+}
+
+hipError_t launch_stageb(const StageBArgs &a, int emax, hipStream_t stream) {
+    if (a.groups <= 0 || emax <= 0) return hipSuccess;
+    dim3 grid(static_cast<unsigned>((a.geo.nq + 63) / 64) * a.groups, (emax + 31) / 32, 1);
+    hipLaunchKernelGGL(stageb_snip, grid, dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace sh

@@ -214,11 +214,43 @@ def gen_config(k, m):
     return path
 
 
+# Snippet table for runtime coefficients (decode stage B, csrc/stageb.hip): snippet c computes
+# tmp[b] = T0[lo(c*2^b)] ^ T1[hi(c*2^b)], b = 0..7, from window tables pinned in VGPRs, and
+# returns with s_setpc_b64. 256 snippets x 64 B = 16 KB, emitted inside the kernel behind an
+# s_branch (file-scope asm is dropped by HIP device compilation).
+SNIP_T0, SNIP_T1, SNIP_TMP = 100, 116, 132
+
+
+def gen_snippets():
+    lines = ["// GENERATED by tools/gen_fixed_kernels.py -- do not edit.",
+             "// 256 compile-time 'multiply by c' snippets (see csrc/stageb.hip).",
+             "#pragma once",
+             f"#define SH_SNIP_T0 {SNIP_T0}",
+             f"#define SH_SNIP_T1 {SNIP_T1}",
+             f"#define SH_SNIP_TMP {SNIP_TMP}",
+             '#define SH_SNIPPET_TABLE(SFX) asm volatile("s_branch sh_snip_end" #SFX "\\n"',
+             '    ".p2align 6\\n"',
+             '    "sh_snip_base" #SFX ":\\n"']
+    for c in range(256):
+        v = c
+        lines.append('    ".p2align 6\\n"')
+        for b in range(8):
+            lo, hi = v & 15, v >> 4
+            lines.append(f'    "v_xor_b32 v{SNIP_TMP + b}, v{SNIP_T0 + lo}, v{SNIP_T1 + hi}\\n"')
+            v = gmul(v, 2)
+        lines.append('    "s_setpc_b64 s[40:41]\\n"')
+    lines.append('    "sh_snip_end" #SFX ":\\n" ::: "memory")')
+    with open(os.path.join(OUTDIR, "snippets.h"), "w") as f:
+        f.write(lines[0] + "\n" + lines[1] + "\n" + lines[2] + "\n" + "\n".join(lines[3:6]) + "\n"
+                + " \\\n".join(lines[6:]) + "\n")
+
+
 def main(argv=()):
     cfgs = CONFIGS
     if argv:
         cfgs = [tuple(map(int, a.split(","))) for a in argv]
     paths = [gen_config(k, m) for (k, m) in cfgs]
+    gen_snippets()
     # registry of generated shapes
     reg = ["// GENERATED by tools/gen_fixed_kernels.py -- list of compile-time-scheduled (k, m).",
            "#pragma once", "#define SH_FIXED_CONFIGS(X) \\"]
