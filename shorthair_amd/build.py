@@ -26,6 +26,8 @@ def generate():
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     os.makedirs(GEN_DIR, exist_ok=True)
+    for f in os.listdir(GEN_DIR):  # drop outputs of earlier generator versions
+        os.remove(os.path.join(GEN_DIR, f))
     mod.OUTDIR = GEN_DIR
     mod.main([])
 
@@ -45,6 +47,7 @@ def _stale():
 
 
 FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result"]
+FLAGS += os.environ.get("SH_EXTRA_FLAGS", "").split()  # experiments only (tools/build_variant.sh)
 OBJ_DIR = os.path.join(HERE, os.environ.get("SH_OBJ_DIR", "build_obj"))
 
 
@@ -52,6 +55,7 @@ def _compile(src, verbose):
     obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(
             os.path.getmtime(src), os.path.getmtime(os.path.join(CSRC, "fixed_common.hpp")),
+            *( [os.path.getmtime(src[:-8] + ".inc")] if src.endswith(("_enc.hip", "_dec.hip")) else []),
             os.path.getmtime(os.path.join(CSRC, "kernels.hpp"))):
         return obj, None
     cmd = [HIPCC] + FLAGS + [f"-I{GEN_DIR}", "-c", src, "-o", obj]

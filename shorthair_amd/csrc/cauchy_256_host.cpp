@@ -155,32 +155,23 @@ uint8_t *generator(Context &c, int k, int m) {
 // Batched calls take the caller's stream verbatim (NULL = the null stream, as in HIP itself).
 hipStream_t pick(void *stream) { return static_cast<hipStream_t>(stream); }
 
-// Compile-time-scheduled kernels address one launch's input/output with 32-bit buffer offsets:
-// split the batch so every launch spans < 2 GiB on each side.
-hipError_t launch_fixed_chunked(int k, int m, int B, int groups, const uint8_t *in, long long in_gs,
-                                uint8_t *out, long long out_gs, const uint8_t *pos,
-                                const uint8_t *rpos, bool dec, hipStream_t s) {
-    const long long limit = (1ll << 31) - (1ll << 24);
-    const long long per = std::max(in_gs, out_gs);
-    const int chunk = static_cast<int>(std::max(1ll, std::min<long long>(groups, limit / per)));
-    const int KP = round4(k), MP = round4(m);
-    for (int g0 = 0; g0 < groups; g0 += chunk) {
-        sh::FixedArgs a{};
-        const int n = std::min(chunk, groups - g0);
-        a.in = in + g0 * in_gs;
-        a.in_gstride = in_gs;
-        a.in_bytes = n * in_gs;
-        a.out = out + g0 * out_gs;
-        a.out_gstride = out_gs;
-        a.out_bytes = n * out_gs;
-        a.groups = n;
-        a.geo = sh::make_geometry(B);
-        a.pos = pos ? pos + static_cast<long long>(g0) * KP : nullptr;
-        a.rpos = rpos ? rpos + static_cast<long long>(g0) * MP : nullptr;
-        hipError_t e = sh::launch_fixed(k, m, a, dec, s);
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
+// One launch of a compile-time-scheduled kernel over the whole batch (the kernels build their
+// buffer descriptors per workgroup, so 32-bit offsets never limit the batch size).
+hipError_t launch_fixed_batch(int k, int m, int B, int groups, const uint8_t *in, long long in_gs,
+                              uint8_t *out, long long out_gs, const uint8_t *pos,
+                              const uint8_t *rpos, bool dec, hipStream_t s) {
+    sh::FixedArgs a{};
+    a.in = in;
+    a.in_gstride = in_gs;
+    a.in_bytes = static_cast<long long>(groups) * in_gs;
+    a.out = out;
+    a.out_gstride = out_gs;
+    a.out_bytes = static_cast<long long>(groups) * out_gs;
+    a.groups = groups;
+    a.geo = sh::make_geometry(B);
+    a.pos = pos;
+    a.rpos = rpos;
+    return sh::launch_fixed(k, m, a, dec, s);
 }
 
 // ---- batched encode ----
@@ -202,7 +193,8 @@ int encode_batch(int k, int m, int B, int groups, const uint8_t *d_in, uint8_t *
         return (m == 1 || valid) ? 0 : -1;  // m == 1 returns before validation (:1503-1506)
     }
     if (sh::has_fixed(k, m, B)) {
-        SH_CHECK(launch_fixed_chunked(k, m, B, groups, d_in, in_gs, d_out, out_gs, nullptr, nullptr, false, s));
+        SH_CHECK(launch_fixed_batch(k, m, B, groups, d_in, in_gs, d_out, out_gs, nullptr, nullptr,
+                                    false, s));
         return 0;
     }
     uint8_t *gen = generator(c, k, m);
@@ -314,7 +306,7 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
     if (w.fixed) {
         // Stage A (compile-time generator, all m rows, erased columns read as zeros):
         //   residual_y = R_y + sum_{received x} M(C[y][x]) d_x
-        SH_CHECK(launch_fixed_chunked(k, m, B, groups, d_blocks, static_cast<long long>(k) * B,
+        SH_CHECK(launch_fixed_batch(k, m, B, groups, d_blocks, static_cast<long long>(k) * B,
                                       w.residual, static_cast<long long>(m) * B, w.pos, w.rpos, true, s));
         // Stage B: recovered_j = sum_y M(S^-1[j][i(y)]) residual_y over the received rows y
         SH_CHECK(launch_stage_b(c, w, m, B, groups, dst, s));

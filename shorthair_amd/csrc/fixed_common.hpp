@@ -1,14 +1,40 @@
 // Common scaffolding for the compile-time-scheduled kernels generated into csrc/gen/.
 //
-// A generated file defines `body_<name>(part, src, acc)` -- straight-line window-table XORs with
-// the generator coefficients baked in -- and ends with FIXED_KERNELS(name, K, M, P), which
-// instantiates the encode and decode-stage-A kernels and their launcher here.
+// A generated file (fixed_<name>.inc) defines `run_<name>_p<p>(src, sink)` -- straight-line
+// window-table XORs with the generator coefficients baked in, one step per input block -- and
+// fixed_<name>_{enc,dec}.hip instantiate one kernel each through FIXED_KERNEL below.
 //
-// Work decomposition: lanes are flattened over (group g, word column q) exactly like the generic
-// kernel (each lane runs the whole group's bitmatrix on its 32 bit-columns). A workgroup of 256
-// threads holds CS = 4/P column sets of 64 lanes; its P waves per column set each produce one
-// part (<= 16 rows) of the output, so the part waves read the same input words back to back
-// (L1/L2 hits) instead of re-streaming them from HBM.
+// Work decomposition. Lanes are flattened over (group g, word column q): a lane owns bytes
+// 4q..4q+3 of all 8 sub-blocks of a group ("bitsliced": each bit position is an independent
+// column of the bitmatrix product). A workgroup covers COLS = CW*64 consecutive columns with
+// CW column-waves x P part-waves; part p produces output rows [p*rows, (p+1)*rows). The CW waves
+// of one part execute the same straight-line code in lockstep, sharing instruction fetch.
+//
+// Input staging (LDS ring, filled by LDS-DMA). Input block x of all the workgroup's columns is
+// one ring slot laid out [sub-block a][column c] (words), so a lane's 8 words of step x are 8
+// conflict-free ds_read_b32 at compile-time offsets. The slot is filled by `buffer_load_dwordx4
+// ... lds`: per-lane global source addresses gather each sub-block's (at B=1400: 175-byte) span
+// into the aligned LDS image, so misalignment costs nothing in the compute loop. Measured on
+// gfx950 (tools/dma_probe.hip): misaligned LDS-DMA sources are exact; a dword straddling the
+// buffer's num_records reads as 0.
+//
+// Pipeline (R slots). Iteration x: wait (counted vmcnt) for this wave's DMA of step x+1, join
+// the workgroup barrier (every wave's share of slot x+1 has landed, and every wave has finished
+// computing step x-1, so slot x-1 is free), issue the ds_reads of step x+1 into the second
+// register set, issue the DMA of step x+R-1 into slot x-1, then compute step x from the
+// registers read one iteration earlier: the LDS read latency hides under the compute, R-2 DMA
+// steps stay in flight. All P part-waves read the same slot: HBM sees each input byte once.
+//
+// Sub-block tails. When sub = B/8 is not a multiple of 4 (175 at B = 1400) the last 4-column
+// chunk of every sub-block is shifted back by shift = 4*nq - sub bytes, on input (DMA source)
+// and output (store offset) alike: its 4 lanes compute bytes [sub-16, sub) instead of
+// [4nq-16, 4nq). Every word a lane computes is then a real column, every store is a plain dword
+// store, nothing reads or writes past a sub-block, and the first shift bytes of the chunk are
+// written twice with identical values (also by the column before it).
+//
+// Addressing. Buffer descriptors are built per workgroup with the base at the workgroup's first
+// group, so 32-bit offsets cover any batch (no 2 GiB launch split); num_records stops at the end
+// of the batch.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -28,45 +54,9 @@ namespace fixed {
 // 2-input XOR as a bitop3 (third operand ignored): opaque to LLVM's reassociation.
 #define X2(a, b) __builtin_amdgcn_bitop3_b32((a), (b), (a), 0x3C)
 
-// What the sources need from FixedArgs, in 32-bit units (one launch's input spans < 2 GiB; the
-// host splits larger batches into several launches).
-struct FixedArgsView {
-    const uint8_t *in;
-    uint32_t in_bytes;
-    uint32_t in_gstride;
-    uint32_t B;
-    uint32_t sub;
-};
+typedef __attribute__((address_space(3))) void lds_void;
+constexpr uint32_t OOR = 0x80000000u;  // buffer offset past every descriptor's range (< 2 GiB)
 
-__device__ __forceinline__ uint32_t ldw(const uint8_t *p) {
-    uint32_t w;
-    __builtin_memcpy(&w, p, 4);
-    return w;
-}
-
-__device__ __forceinline__ void stw(uint8_t *p, uint32_t w) { __builtin_memcpy(p, &w, 4); }
-
-// Per-lane column geometry. A lane owns bytes 4q..4q+3 of every sub-block. The last word of a
-// sub-block holds `tail` < 4 valid bytes when sub % 4 != 0; loading it whole over-reads into the
-// next sub-block, which only pollutes bit-columns that are never stored -- harmless, except past
-// the end of the whole input buffer. So only the LAST group's tail lane loads sub-block 7
-// shifted back by (4 - tail) bytes and shifts the word into place (shr7).
-struct Col {
-    int q;
-    int nbytes;     // bytes this lane stores per sub-block (1..4)
-    int back7;      // bytes the sub-block-7 load is shifted back (last group's tail lane only)
-};
-
-__device__ __forceinline__ Col make_col(int g, int q, int groups, const Geometry &geo) {
-    Col c;
-    c.q = q;
-    const bool tail = (q == geo.nq - 1) && geo.tail < 4;
-    c.nbytes = tail ? geo.tail : 4;
-    c.back7 = (tail && g == groups - 1) ? 4 - geo.tail : 0;
-    return c;
-}
-
-// Buffer descriptor over one launch's input: raw (stride 0) buffer, `bytes` records.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const uint8_t *p, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p), static_cast<short>(0),
                                              static_cast<int>(bytes), 0x00020000);
@@ -76,197 +66,261 @@ __device__ __forceinline__ uint32_t bload(__amdgpu_buffer_rsrc_t r, uint32_t vof
     return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
 }
 
-// Encode source: block x of group g = in + g*gstride + x*B. Per-lane offsets of the 8 sub-block
-// words are computed once (voff[a]); the per-step block offset x*B is a scalar (soffset), so a
-// step's 8 loads cost no vector ALU at all.
-template <int K>
-struct EncSrc {
-    __amdgpu_buffer_rsrc_t rsrc;
-    uint32_t voff[8];
-    uint32_t voff7_last;  // sub-block 7 of the LAST block, shifted back on the buffer-end lane
-    uint32_t B;
-    uint32_t shr7;
-    __device__ __forceinline__ void init(const FixedArgsView &v, int g, const Col &c) {
-        rsrc = make_rsrc(v.in, v.in_bytes);
-        B = v.B;
-        const uint32_t base = static_cast<uint32_t>(g) * v.in_gstride + 4u * c.q;
-#pragma unroll
-        for (int a = 0; a < 8; ++a) voff[a] = base + a * v.sub;
-        voff7_last = voff[7] - c.back7;
-        shr7 = 8u * c.back7;
-    }
-    __device__ __forceinline__ void load(int x, uint32_t &d0, uint32_t &d1, uint32_t &d2,
-                                         uint32_t &d3, uint32_t &d4, uint32_t &d5, uint32_t &d6,
-                                         uint32_t &d7) const {
-        const uint32_t s = static_cast<uint32_t>(x) * B;
-        d0 = bload(rsrc, voff[0], s);
-        d1 = bload(rsrc, voff[1], s);
-        d2 = bload(rsrc, voff[2], s);
-        d3 = bload(rsrc, voff[3], s);
-        d4 = bload(rsrc, voff[4], s);
-        d5 = bload(rsrc, voff[5], s);
-        d6 = bload(rsrc, voff[6], s);
-        d7 = bload(rsrc, x == K - 1 ? voff7_last : voff[7], s);
-    }
-    // Only the last block of the buffer can be over-read past its end (x == K-1).
-    __device__ __forceinline__ uint32_t fix7(int x, uint32_t d7) const {
-        return x == K - 1 ? d7 >> shr7 : d7;
-    }
-    __device__ __forceinline__ void add_row(int, uint32_t (&)[8]) const {}
+// Descriptor over [base + first*gstride, base + total) capped below 2 GiB.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wg_rsrc(const uint8_t *base, long long total,
+                                                          long long gstride, int first) {
+    const long long start = static_cast<long long>(first) * gstride;
+    long long n = total - start;
+    n = n < 0 ? 0 : (n > 0x7FFFFFFFll ? 0x7FFFFFFFll : n);
+    return make_rsrc(base + start, static_cast<uint32_t>(n));
+}
+
+// Compile-time shape of one kernel instance.
+template <int K_, int M_, int P_, int CW_, int R_>
+struct Shape {
+    static constexpr int K = K_, M = M_, P = P_, CW = CW_, R = R_, W = 16;
+    static constexpr int NW = CW * P, NT = 64 * NW, COLS = CW * 64;
+    static constexpr int ROWB = COLS * 4;               // bytes of one sub-block row of a slot
+    static constexpr int SLOT = 8 * ROWB;               // bytes per ring slot (one input block)
+    static constexpr int NDMA = SLOT / (64 * W);        // DMA wave-instructions per step
+    static constexpr int DPW = (NDMA + NW - 1) / NW;    // ... issued by each wave (at most)
+    static constexpr int KP = (K + 3) & ~3, MP = (M + 3) & ~3;
+    static_assert(R >= 3 && R * SLOT <= 65536, "ring must fit ds_read's 16-bit offsets");
 };
 
-// Decode stage-A source: original row x sits at array index pos[x] of the group's received
-// blocks (pos in LDS), or is erased (0xFF): then the offset is pushed out of the buffer's range
-// and the buffer load returns zeros. Per step: one LDS byte read + one multiply-add per lane;
-// the sub-block offset a*sub is the scalar operand.
-template <int K>
-struct DecSrc {
-    __amdgpu_buffer_rsrc_t rsrc;
-    uint32_t base;      // g*gstride + 4q
-    uint32_t soff[8];   // a*sub (uniform)
-    uint32_t B;
-    uint32_t shr7;
-    int back7;
-    const uint8_t *pos;
-    __device__ __forceinline__ void init(const FixedArgsView &v, int g, const Col &c,
-                                         const uint8_t *lds_pos, int kp) {
-        KP_OFF = kp;
-        rsrc = make_rsrc(v.in, v.in_bytes);
-        B = v.B;
-        base = static_cast<uint32_t>(g) * v.in_gstride + 4u * c.q;
-#pragma unroll
-        for (int a = 0; a < 8; ++a) soff[a] = a * v.sub;
-        back7 = c.back7;
-        shr7 = 8u * c.back7;
-        pos = lds_pos;
-    }
-    __device__ __forceinline__ uint32_t block_off(int p) const {
-        return p == 0xFF ? 0x80000000u : base + static_cast<uint32_t>(p) * B;
-    }
-    __device__ __forceinline__ void load(int x, uint32_t &d0, uint32_t &d1, uint32_t &d2,
-                                         uint32_t &d3, uint32_t &d4, uint32_t &d5, uint32_t &d6,
-                                         uint32_t &d7) const {
-        const uint32_t o = block_off(pos[x]);
-        d0 = bload(rsrc, o, soff[0]);
-        d1 = bload(rsrc, o, soff[1]);
-        d2 = bload(rsrc, o, soff[2]);
-        d3 = bload(rsrc, o, soff[3]);
-        d4 = bload(rsrc, o, soff[4]);
-        d5 = bload(rsrc, o, soff[5]);
-        d6 = bload(rsrc, o, soff[6]);
-        d7 = bload(rsrc, o - back7, soff[7]);
-    }
-    __device__ __forceinline__ uint32_t fix7(int, uint32_t d7) const { return d7 >> shr7; }
-    // acc ^= the received recovery block of generator row y (zeros when row y is absent).
-    __device__ __forceinline__ void add_row(int y, uint32_t (&acc)[8]) const {
-        const uint32_t o = block_off(pos[KP_OFF + y]);
-#pragma unroll
-        for (int a = 0; a < 7; ++a) acc[a] = X2(acc[a], bload(rsrc, o, soff[a]));
-        acc[7] = X2(acc[7], bload(rsrc, o - back7, soff[7]) >> shr7);
-    }
-    int KP_OFF;
+// Per-lane geometry shared by the source and the sink.
+struct WGInfo {
+    long long col0;  // first column of the workgroup
+    int g_first;     // group of col0 (descriptor base)
+    int wave, lane, c;
+    int gl, q;       // this lane's group (relative to g_first) and word column
+    bool valid;      // g < groups
 };
 
-// Branch-free output: every lane issues a dword store, a short store and a byte store per output
-// word; the ones a lane must not perform get an out-of-range offset and are dropped by the
-// buffer unit. Normal lanes store the dword; a sub-block's short last word (tail = 1..3 valid
-// bytes) is stored as short and/or byte. No branches -> the whole part stays one basic block,
-// which keeps LLVM from sinking the accumulator updates into the epilogue.
-struct Sink {
+// Input side. DMA instruction i = wave*DPW + j covers slot bytes [i*1024, (i+1)*1024): lane byte
+// `off` -> sub-block a = off / ROWB, first column cc = (off % ROWB) / 4, a 4-column chunk that
+// lies in one group because nq % 4 == 0 (has_fixed).
+// Byte offset of word column q inside a sub-block (the last chunk shifted back, see above).
+__device__ __forceinline__ uint32_t col_off(int q, const Geometry &geo) {
+    return 4u * q - (q >= geo.nq - 4 ? static_cast<uint32_t>(4 * geo.nq - geo.sub) : 0u);
+}
+
+template <class S, bool DEC>
+struct Src {
     __amdgpu_buffer_rsrc_t rsrc;
-    uint32_t v_dw, v_sh, v_b8;  // per-lane offsets (or out of range)
-    uint32_t b8_shr;            // byte store takes bits [b8_shr, b8_shr+8)
+    uint32_t dbase[S::DPW];   // chunk source offset, block 0 / array slot 0 (OOR past the batch)
+    int dgl[S::DPW];          // decode: the chunk's group (position-table index)
     uint32_t B, sub;
-    bool has_tail;
-    __device__ __forceinline__ void init(uint8_t *out, uint32_t out_bytes, uint32_t gstride,
-                                         int g, const Col &c, const Geometry &geo) {
-        rsrc = make_rsrc(out, out_bytes);
+    int wave;
+    uint32_t rd;              // this lane's read offset in a slot (c * 4)
+    uint32_t lbase;           // decode epilogue: gl * gstride + col_off(q)
+    int gl;
+    const uint8_t *lds;       // ring base
+    const uint8_t *pos;       // decode: [groups_per_wg][KP + MP] position tables (LDS)
+
+    __device__ __forceinline__ void init(const FixedArgs &a, const WGInfo &w, const uint8_t *lds_ring,
+                                         const uint8_t *lds_pos) {
+        const Geometry &geo = a.geo;
+        rsrc = wg_rsrc(a.in, a.in_bytes, a.in_gstride, w.g_first);
         B = geo.B;
         sub = geo.sub;
-        has_tail = geo.tail < 4;
-        const uint32_t base = static_cast<uint32_t>(g) * gstride + 4u * c.q;
-        const uint32_t OOR = 0x80000000u;
-        const bool t = c.nbytes < 4;
-        v_dw = t ? OOR : base;
-        v_sh = (t && c.nbytes >= 2) ? base : OOR;
-        v_b8 = (t && (c.nbytes & 1)) ? base + (c.nbytes == 3 ? 2u : 0u) : OOR;
-        b8_shr = c.nbytes == 3 ? 16u : 0u;
+        lds = lds_ring;
+        pos = lds_pos;
+        wave = w.wave;
+        rd = static_cast<uint32_t>(w.c) * 4u;
+        const uint32_t gstride = static_cast<uint32_t>(a.in_gstride);
+        gl = w.gl;
+        lbase = static_cast<uint32_t>(w.gl) * gstride + col_off(w.q, geo);
+#pragma unroll
+        for (int j = 0; j < S::DPW; ++j) {
+            const int off = (w.wave * S::DPW + j) * 64 * S::W + w.lane * S::W;
+            const int aa = off / S::ROWB;
+            const int cc = (off - aa * S::ROWB) / 4;
+            const long long colx = w.col0 + cc;
+            const int gx = static_cast<int>(colx / geo.nq);
+            const int qx = static_cast<int>(colx - static_cast<long long>(gx) * geo.nq);
+            dgl[j] = gx - w.g_first;
+            dbase[j] = gx < a.groups
+                           ? static_cast<uint32_t>(gx - w.g_first) * gstride + col_off(qx, geo) + aa * geo.sub
+                           : OOR;
+        }
     }
-    __device__ __forceinline__ void store(int y, int b, uint32_t w) const {
-        const uint32_t so = static_cast<uint32_t>(y) * B + static_cast<uint32_t>(b) * sub;
-        __builtin_amdgcn_raw_buffer_store_b32(w, rsrc, v_dw, so, 0);
-        if (has_tail) {  // uniform
-            __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(w), rsrc, v_sh, so, 0);
-            __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(w >> b8_shr), rsrc, v_b8, so, 0);
+
+    // Wait until this wave's DMAs of steps <= T are done (I = steps issued so far), then join the
+    // workgroup barrier. One asm statement: nothing is scheduled between the two.
+    template <int T, int I>
+    __device__ __forceinline__ static void wait() {
+        constexpr int N = (I - T - 1) * S::DPW;
+        static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+    }
+
+    // Decode: the DMA source of step x depends on the group's position table (LDS). pre(x) reads
+    // it one iteration before issue(x, .) needs it, so the DMA issue never waits on LDS latency.
+    struct Pre {
+        int p[S::DPW];
+    };
+    __device__ __forceinline__ Pre pre(int x) const {
+        Pre r;
+#pragma unroll
+        for (int j = 0; j < S::DPW; ++j) r.p[j] = DEC ? pos[dgl[j] * (S::KP + S::MP) + x] : 0;
+        return r;
+    }
+
+    // DMA of input step x into its ring slot.
+    __device__ __forceinline__ void issue(int x, const Pre &pr) const {
+        uint8_t *slot = const_cast<uint8_t *>(lds) + (x % S::R) * S::SLOT;
+#pragma unroll
+        for (int j = 0; j < S::DPW; ++j) {
+            if (S::NDMA % S::NW != 0 && wave * S::DPW + j >= S::NDMA) break;  // uniform
+            lds_void *dst = (lds_void *)(slot + (wave * S::DPW + j) * 64 * S::W);
+            if (DEC) {
+                const int p = pr.p[j];
+                const uint32_t o = (p == 0xFF || dbase[j] == OOR) ? OOR : dbase[j] + static_cast<uint32_t>(p) * B;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, S::W, o, 0, 0, 0);
+            } else {
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, S::W, dbase[j],
+                                                         static_cast<uint32_t>(x) * B, 0, 0);
+            }
+        }
+    }
+
+    __device__ __forceinline__ void read(int slot, uint32_t &d0, uint32_t &d1, uint32_t &d2,
+                                         uint32_t &d3, uint32_t &d4, uint32_t &d5, uint32_t &d6,
+                                         uint32_t &d7) const {
+        const uint8_t *p = lds + slot * S::SLOT + rd;
+        d0 = *reinterpret_cast<const uint32_t *>(p + 0 * S::ROWB);
+        d1 = *reinterpret_cast<const uint32_t *>(p + 1 * S::ROWB);
+        d2 = *reinterpret_cast<const uint32_t *>(p + 2 * S::ROWB);
+        d3 = *reinterpret_cast<const uint32_t *>(p + 3 * S::ROWB);
+        d4 = *reinterpret_cast<const uint32_t *>(p + 4 * S::ROWB);
+        d5 = *reinterpret_cast<const uint32_t *>(p + 5 * S::ROWB);
+        d6 = *reinterpret_cast<const uint32_t *>(p + 6 * S::ROWB);
+        d7 = *reinterpret_cast<const uint32_t *>(p + 7 * S::ROWB);
+    }
+
+    // Epilogue for output rows Y0..Y0+NR-1 of this part (decode only): acc ^= the received
+    // recovery block of generator row y (zeros when absent); all loads of a batch of rows are
+    // issued before the first XOR (one memory round trip per batch).
+    template <int Y0, int NR>
+    __device__ __forceinline__ void epilogue(uint32_t (&acc)[NR][8]) const {
+        if (!DEC) return;
+        constexpr int CH = 4;  // rows per batch of loads (register budget)
+#pragma unroll
+        for (int y0 = 0; y0 < NR; y0 += CH) {
+            uint32_t v[CH][8];
+#pragma unroll
+            for (int yi = 0; yi < CH && y0 + yi < NR; ++yi) {
+                const int p = pos[gl * (S::KP + S::MP) + S::KP + Y0 + y0 + yi];
+                const uint32_t o = p == 0xFF ? OOR : lbase + static_cast<uint32_t>(p) * B;
+#pragma unroll
+                for (int aa = 0; aa < 8; ++aa) v[yi][aa] = bload(rsrc, o, aa * sub);
+            }
+#pragma unroll
+            for (int yi = 0; yi < CH && y0 + yi < NR; ++yi)
+#pragma unroll
+                for (int aa = 0; aa < 8; ++aa) acc[y0 + yi][aa] = X2(acc[y0 + yi][aa], v[yi][aa]);
         }
     }
 };
 
+// Output: one dword store per word (the shifted last chunk makes every word a full real one);
+// lanes past the last group get an out-of-range offset, dropped by the buffer unit.
+struct Sink {
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t voff, B, sub;
+    __device__ __forceinline__ void init(const FixedArgs &a, const WGInfo &w) {
+        const Geometry &geo = a.geo;
+        rsrc = wg_rsrc(a.out, a.out_bytes, a.out_gstride, w.g_first);
+        B = geo.B;
+        sub = geo.sub;
+        voff = w.valid ? static_cast<uint32_t>(w.gl) * static_cast<uint32_t>(a.out_gstride) + col_off(w.q, geo)
+                       : OOR;
+    }
+    __device__ __forceinline__ void store(int y, int b, uint32_t w) const {
+#ifdef SH_EXPERIMENT_NO_STORE  // timing experiment only: keep the value, drop the store
+        asm volatile("" ::"v"(w));
+        return;
+#endif
+        __builtin_amdgcn_raw_buffer_store_b32(w, rsrc, voff, static_cast<uint32_t>(y) * B + static_cast<uint32_t>(b) * sub, 0);
+    }
+};
+
+// Sets up src/sink, issues the ring's first R-1 DMAs and returns this wave's part. The caller
+// (the FIXED_KERNEL macro) then calls the generated run_<name> directly, so everything inlines
+// into one function: a non-inlined body took `src` by reference through scratch and read the
+// LDS ring with flat loads.
+template <class S, bool DEC>
+__device__ __forceinline__ int kernel_prologue(const FixedArgs &a, uint8_t *lds, Src<S, DEC> &src,
+                                               Sink &sink) {
+    WGInfo w;
+    w.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    w.lane = threadIdx.x & 63;
+    const int part = w.wave % S::P;
+    const int cw = w.wave / S::P;
+    w.c = cw * 64 + w.lane;
+    w.col0 = static_cast<long long>(blockIdx.x) * S::COLS;
+    const int nq = a.geo.nq;
+    w.g_first = static_cast<int>(w.col0 / nq);
+    const long long col = w.col0 + w.c;
+    const int g = static_cast<int>(col / nq);
+    w.q = static_cast<int>(col - static_cast<long long>(g) * nq);
+    w.gl = g - w.g_first;
+    w.valid = g < a.groups;
+    uint8_t *lds_pos = lds + S::R * S::SLOT;
+    if (DEC) {
+        const int ng = a.groups_per_wg;
+        constexpr int TW = (S::KP + S::MP) / 4;
+        for (int i = threadIdx.x; i < ng * TW; i += S::NT) {
+            const int lg = i / TW, t = i - lg * TW;
+            const int gg = w.g_first + lg;
+            uint32_t v = 0xFFFFFFFFu;
+            if (gg < a.groups) {
+                v = (t < S::KP / 4)
+                        ? reinterpret_cast<const uint32_t *>(a.pos + gg * static_cast<long long>(S::KP))[t]
+                        : reinterpret_cast<const uint32_t *>(a.rpos + gg * static_cast<long long>(S::MP))[t - S::KP / 4];
+            }
+            reinterpret_cast<uint32_t *>(lds_pos)[i] = v;
+        }
+        __syncthreads();
+    }
+    src.init(a, w, lds, lds_pos);
+    sink.init(a, w);
+#pragma unroll
+    for (int x = 0; x < S::R - 1 && x < S::K; ++x) src.issue(x, src.pre(x));
+    return part;
+}
+
+template <class S>
+inline hipError_t launch_shape(FixedArgs a, bool dec, hipStream_t s, void (*kern)(FixedArgs)) {
+    a.groups_per_wg = (S::COLS - 1) / a.geo.nq + 2;
+    const long long cols = static_cast<long long>(a.groups) * a.geo.nq;
+    const unsigned blocks = static_cast<unsigned>((cols + S::COLS - 1) / S::COLS);
+    const size_t lds = static_cast<size_t>(S::R) * S::SLOT +
+                       (dec ? static_cast<size_t>(a.groups_per_wg) * (S::KP + S::MP) : 0);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(S::NT), lds, s, a);
+    return hipGetLastError();
+}
+
 }  // namespace fixed
 }  // namespace sh
 
-// Kernel + launcher for one generated (k, m). LDS: decode position tables of the groups a
-// workgroup touches ([groups_per_wg][round4(K) + round4(M)] bytes).
-#define FIXED_KERNELS(NAME, K, M, P, RPP)                                                            \
+// One kernel + launcher of a generated (k, m): MODE enc (DEC = false) or dec (DEC = true);
+// MINW = waves per SIMD the registers are allocated for. The host routes shapes with
+// nq % 4 != 0 (a 16-byte chunk could straddle two groups) or sub < 16 to the generic kernel.
+#define FIXED_KERNEL(NAME, K, M, P, CW, R, MINW, MODE, DEC)                                       \
     namespace sh {                                                                                \
     namespace fixed {                                                                             \
-    template <bool DEC>                                                                           \
-    __global__ __launch_bounds__(256) void kern_##NAME(FixedArgs a) {                             \
-        constexpr int CS = (P >= 4) ? 1 : 4 / P;                                                  \
-        constexpr int KP = (K + 3) & ~3, MP = (M + 3) & ~3;                                       \
+    __global__ __launch_bounds__(64 * CW * P, MINW) void kern_##NAME##_##MODE(FixedArgs a) {      \
         extern __shared__ __attribute__((aligned(16))) uint8_t lds[];                             \
-        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);                        \
-        const int lane = threadIdx.x & 63;                                                        \
-        const int part = wave % P;                                                                \
-        const long long col0 = static_cast<long long>(blockIdx.x) * CS * 64;                      \
-        const long long col = col0 + (wave / P) * 64 + lane;                                      \
-        const int g = static_cast<int>(col / a.geo.nq);                                           \
-        const int q = static_cast<int>(col - static_cast<long long>(g) * a.geo.nq);               \
-        const int g_first = static_cast<int>(col0 / a.geo.nq);                                    \
-        if (DEC) {                                                                                \
-            const int ng = a.groups_per_wg;                                                       \
-            for (int i = threadIdx.x; i < ng * (KP + MP) / 4; i += blockDim.x) {                  \
-                const int lg = i / ((KP + MP) / 4), w = i - lg * ((KP + MP) / 4);                 \
-                const int gg = g_first + lg;                                                      \
-                uint32_t v = 0xFFFFFFFFu;                                                         \
-                if (gg < a.groups) {                                                              \
-                    v = (w < KP / 4) ? reinterpret_cast<const uint32_t *>(a.pos + gg * (long long)KP)[w] \
-                                     : reinterpret_cast<const uint32_t *>(a.rpos + gg * (long long)MP)[w - KP / 4]; \
-                }                                                                                 \
-                reinterpret_cast<uint32_t *>(lds)[i] = v;                                         \
-            }                                                                                     \
-            __syncthreads();                                                                      \
-        }                                                                                         \
-        if (g >= a.groups) return;                                                                \
-        const Geometry geo = a.geo;                                                               \
-        const Col c = make_col(g, q, a.groups, geo);                                              \
-        const FixedArgsView v{a.in, static_cast<uint32_t>(a.in_bytes),                            \
-                              static_cast<uint32_t>(a.in_gstride), static_cast<uint32_t>(geo.B),  \
-                              static_cast<uint32_t>(geo.sub)};                                    \
+        using S = Shape<K, M, P, CW, R>;                                                          \
+        Src<S, DEC> src;                                                                          \
         Sink sink;                                                                                \
-        sink.init(a.out, static_cast<uint32_t>(a.out_bytes), static_cast<uint32_t>(a.out_gstride), \
-                  g, c, geo);                                                                     \
-        if (DEC) {                                                                                \
-            DecSrc<K> src;                                                                        \
-            src.init(v, g, c, lds + (g - g_first) * (KP + MP), KP);                               \
-            run_##NAME(part, src, sink);                                                          \
-        } else {                                                                                  \
-            EncSrc<K> src;                                                                        \
-            src.init(v, g, c);                                                                    \
-            run_##NAME(part, src, sink);                                                          \
-        }                                                                                         \
+        const int part = kernel_prologue<S, DEC>(a, lds, src, sink);                              \
+        run_##NAME(part, src, sink);                                                              \
     }                                                                                             \
-    hipError_t launch_##NAME(FixedArgs a, bool dec, hipStream_t s) {                              \
-        constexpr int CS = (P >= 4) ? 1 : 4 / P;                                                  \
-        a.groups_per_wg = (CS * 64 - 1) / a.geo.nq + 2;                                           \
-        const long long cols = static_cast<long long>(a.groups) * a.geo.nq;                       \
-        const unsigned blocks = static_cast<unsigned>((cols + CS * 64 - 1) / (CS * 64));           \
-        const size_t lds = dec ? static_cast<size_t>(a.groups_per_wg) * (((K + 3) & ~3) + ((M + 3) & ~3)) : 0; \
-        if (dec)                                                                                  \
-            hipLaunchKernelGGL(kern_##NAME<true>, dim3(blocks), dim3(CS * P * 64), lds, s, a);    \
-        else                                                                                      \
-            hipLaunchKernelGGL(kern_##NAME<false>, dim3(blocks), dim3(CS * P * 64), lds, s, a);   \
-        return hipGetLastError();                                                                 \
+    hipError_t launch_##NAME##_##MODE(FixedArgs a, hipStream_t s) {                               \
+        return launch_shape<Shape<K, M, P, CW, R>>(a, DEC, s, kern_##NAME##_##MODE);              \
     }                                                                                             \
     }                                                                                             \
     }

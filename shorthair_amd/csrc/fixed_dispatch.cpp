@@ -6,13 +6,17 @@
 
 namespace sh {
 namespace fixed {
-#define SH_DECL(K, M) hipError_t launch_k##K##_m##M(FixedArgs a, bool dec, hipStream_t s);
+#define SH_DECL(K, M)                                                    \
+    hipError_t launch_k##K##_m##M##_enc(FixedArgs a, hipStream_t s);     \
+    hipError_t launch_k##K##_m##M##_dec(FixedArgs a, hipStream_t s);
 SH_FIXED_CONFIGS(SH_DECL)
 #undef SH_DECL
 }  // namespace fixed
 
 bool has_fixed(int k, int m, int B) {
-    if (B % 8 != 0 || B / 8 < 4) return false;
+    // 16-byte DMA chunks must not straddle two groups (nq = ceil(B/8 / 4) % 4 == 0) and the
+    // shifted last chunk must stay inside its sub-block (B/8 >= 16); see fixed_common.hpp.
+    if (B % 8 != 0 || B / 8 < 16 || ((B / 8 + 3) / 4) % 4 != 0) return false;
 #define SH_HAS(K, M) if (k == K && m == M) return true;
     SH_FIXED_CONFIGS(SH_HAS)
 #undef SH_HAS
@@ -22,7 +26,9 @@ bool has_fixed(int k, int m, int B) {
 hipError_t launch_fixed(int k, int m, FixedArgs a, bool dec, hipStream_t stream) {
     if (!has_fixed(k, m, a.geo.B)) return hipErrorNotSupported;
     if (a.groups <= 0) return hipSuccess;
-#define SH_GO(K, M) if (k == K && m == M) return fixed::launch_k##K##_m##M(a, dec, stream);
+#define SH_GO(K, M)                                                                         \
+    if (k == K && m == M)                                                                   \
+        return dec ? fixed::launch_k##K##_m##M##_dec(a, stream) : fixed::launch_k##K##_m##M##_enc(a, stream);
     SH_FIXED_CONFIGS(SH_GO)
 #undef SH_GO
     return hipErrorNotSupported;

@@ -103,15 +103,14 @@ hipError_t launch_stageb(const StageBArgs &a, int emax, hipStream_t stream);
 struct FixedArgs {
     const uint8_t *in;        // encode: data [G][k][B]; decode A: received blocks [G][k][B]
     long long in_gstride;
-    long long in_bytes;       // groups * in_gstride (< 2 GiB per launch; the host splits)
+    long long in_bytes;       // groups * in_gstride
     uint8_t *out;             // encode: recovery [G][m][B]; decode A: residual [G][m][B]
     long long out_gstride;
-    long long out_bytes;      // groups * out_gstride (< 2 GiB per launch)
+    long long out_bytes;      // groups * out_gstride
     int groups;
     Geometry geo;
     const uint8_t *pos;       // decode: [G][round4(k)] array index of original row x, 0xFF = erased
     const uint8_t *rpos;      // decode: [G][round4(m)] array index of recovery row y, 0xFF = absent
-    const uint8_t *zero;      // decode: >= B zero bytes
     int groups_per_wg;        // set by the launcher
 };
 

@@ -30,8 +30,7 @@ OUTDIR = os.path.join(ROOT, "shorthair_amd", "csrc", "gen")
 CONFIGS = [(200, 32), (64, 16), (28, 4), (112, 16), (224, 32)]
 if os.environ.get("SH_CONFIGS"):  # experiments: e.g. SH_CONFIGS="200,32;64,16"
     CONFIGS = [tuple(map(int, c.split(","))) for c in os.environ["SH_CONFIGS"].split(";")]
-ROWS_PER_PART = int(os.environ.get("SH_ROWS_PER_PART", "16"))
-PREFETCH = int(os.environ.get("SH_PREFETCH", "2"))
+ROWS_PER_PART = int(os.environ.get("SH_ROWS_PER_PART", "8"))
 
 
 def gf_tables():
@@ -103,9 +102,10 @@ class Body:
         self.k, self.rows, self.y0, self.y1 = k, rows, y0, y1
         self.lines = []
 
-    def table_expr(self, h, v, have):
-        """Name of window-table entry v (1..15) of half h, building it if needed."""
-        base = {1: f"d{4*h+0}", 2: f"d{4*h+1}", 4: f"d{4*h+2}", 8: f"d{4*h+3}"}
+    def table_expr(self, h, v, have, d):
+        """Name of window-table entry v (1..15) of half h, building it if needed (d = name of the
+        register set holding this step's 8 input words)."""
+        base = {1: f"{d}{4*h+0}", 2: f"{d}{4*h+1}", 4: f"{d}{4*h+2}", 8: f"{d}{4*h+3}"}
         if v in base:
             return base[v]
         name = f"t{h}_{v}"
@@ -117,47 +117,60 @@ class Body:
         elif len(bits) == 3:
             self.lines.append(f"    const uint32_t {name} = X3({base[bits[0]]}, {base[bits[1]]}, {base[bits[2]]});")
         else:  # 15 = 3 ^ 12
-            a = self.table_expr(h, 3, have)
-            b = self.table_expr(h, 12, have)
+            a = self.table_expr(h, 3, have, d)
+            b = self.table_expr(h, 12, have, d)
             self.lines.append(f"    const uint32_t {name} = X2({a}, {b});")
         have.add(name)
         return name
 
-    def emit(self, pf=PREFETCH):
-        """Inputs are prefetched `pf` steps ahead into a ring of register sets (raw words; the
-        only per-step fix-up is Src::fix7 for the buffer-end tail lane)."""
+    def emit(self, R):
+        """Software-pipelined steps (see fixed_common.hpp): iteration x waits for slot x+1,
+        reads it into the other register set, refills slot x-1 with block x+R-1, and computes
+        step x from the registers read one iteration earlier. Sets alternate: dA (even x), dB."""
         L = self.lines
         nr = self.y1 - self.y0
-        for s in range(pf):
-            L.append(f"    uint32_t r{s}_0, r{s}_1, r{s}_2, r{s}_3, r{s}_4, r{s}_5, r{s}_6, r{s}_7;")
-        L.append("    uint32_t d0, d1, d2, d3, d4, d5, d6, d7;")
-        for s in range(min(pf, self.k)):
-            L.append(f"    src.load({s}, " + ", ".join(f"r{s}_{a}" for a in range(8)) + ");")
-        for x in range(self.k):
-            slot = x % pf
+        k = self.k
+        L.append("    uint32_t dA0, dA1, dA2, dA3, dA4, dA5, dA6, dA7;")
+        L.append("    uint32_t dB0, dB1, dB2, dB3, dB4, dB5, dB6, dB7;")
+        # prologue: slot 0 (steps 0..R-2 were issued by kernel_prologue)
+        L.append(f"    src.template wait<0, {min(k, R - 1)}>();")
+        L.append("    src.read(0, " + ", ".join(f"dA{a}" for a in range(8)) + ");")
+        if R - 1 < k:
+            L.append(f"    typename Src::Pre pre = src.pre({R - 1});")
+        for x in range(k):
+            cur, nxt = ("dA", "dB") if x % 2 == 0 else ("dB", "dA")
             L.append(f"    // ---- input block {x}")
-            # Pin the step structure: without this hipcc hoists all k steps' loads and address
-            # arithmetic to the top (256 VGPRs + spills, 1 wave/SIMD).
+            # Pin the step structure: without this hipcc hoists work across steps.
             L.append("    __builtin_amdgcn_sched_barrier(0);")
-            L.append("    " + " ".join(f"d{a} = r{slot}_{a};" for a in range(8)))
-            L.append(f"    d7 = src.fix7({x}, d7);")
-            if x + pf < self.k:
-                L.append(f"    src.load({x + pf}, " + ", ".join(f"r{slot}_{a}" for a in range(8)) + ");")
+            if x + 1 < k:
+                issued = min(k, R - 1 + x)
+                L.append(f"    src.template wait<{x + 1}, {issued}>();")
+                L.append(f"    src.read({(x + 1) % R}, " + ", ".join(f"{nxt}{a}" for a in range(8)) + ");")
+                if x + R - 1 < k:
+                    L.append(f"    src.issue({x + R - 1}, pre);")
+                    if x + R < k:
+                        L.append(f"    pre = src.pre({x + R});")
             L.append("    {")
             have = set()
+            # Updates ordered by the high-half table entry: each T1 entry is built right before
+            # the updates that use it and dies after them (fewer live table registers).
+            ups = []
             for yi in range(nr):
-                c = self.rows[self.y0 + yi][x]
-                for b, v in enumerate(row_bytes(c)):
-                    lo, hi = v & 15, v >> 4
-                    acc = f"acc[{yi}][{b}]"
-                    if lo and hi:
-                        ta = self.table_expr(0, lo, have)
-                        tb = self.table_expr(1, hi, have)
-                        L.append(f"    {acc} = X3({acc}, {ta}, {tb});")
-                    elif lo:
-                        L.append(f"    {acc} = X2({acc}, {self.table_expr(0, lo, have)});")
-                    else:
-                        L.append(f"    {acc} = X2({acc}, {self.table_expr(1, hi, have)});")
+                v = self.rows[self.y0 + yi][x]
+                for b in range(8):
+                    ups.append((v >> 4, v & 15, yi, b))
+                    v = gmul(v, 2)
+            ups.sort(key=lambda u: (u[0], u[1]))
+            for hi, lo, yi, b in ups:
+                acc = f"acc[{yi}][{b}]"
+                if lo and hi:
+                    ta = self.table_expr(0, lo, have, cur)
+                    tb = self.table_expr(1, hi, have, cur)
+                    L.append(f"    {acc} = X3({acc}, {ta}, {tb});")
+                elif lo:
+                    L.append(f"    {acc} = X2({acc}, {self.table_expr(0, lo, have, cur)});")
+                else:
+                    L.append(f"    {acc} = X2({acc}, {self.table_expr(1, hi, have, cur)});")
             # Tie every accumulator to this step (an empty volatile asm is a chained side effect):
             # otherwise the DAG scheduler floats the pure bitop3 nodes of a ~30K-node basic block
             # away from their loads and keeps every loaded word live.
@@ -167,20 +180,40 @@ class Body:
         return "\n".join(L)
 
 
+def shape(k, m):
+    """(P parts, CW column waves, R ring slots, waves/SIMD the registers are allocated for).
+    <= ROWS_PER_PART rows per part (8 rows = 64 accumulator VGPRs: ~100 VGPRs, 4 waves/SIMD; the
+    window tables are rebuilt per part, +22 ops per part and step), 4 waves per workgroup."""
+    P = (m + ROWS_PER_PART - 1) // ROWS_PER_PART
+    # Up to 16 waves per workgroup: the CW waves of one part run the SAME straight-line code in
+    # lockstep (one barrier per step), so they share every instruction-cache line they fetch.
+    # (With one wave per part the code stream -- ~0.7 KB per step and part -- outweighs the data
+    # stream and instruction fetch, not HBM, bounds the kernel.)
+    CW = int(os.environ.get("SH_CW", str(max(1, min(8, 16 // P)))))
+    slot = 8 * CW * 64 * 4
+    R = int(os.environ.get("SH_RING", str(max(3, min(8, 65536 // slot)))))
+    rows = (m + P - 1) // P
+    minw = int(os.environ.get("SH_MIN_WAVES", "2" if rows > 12 else ("3" if rows > 8 else "4")))
+    return P, CW, R, minw
+
+
 def gen_config(k, m):
     rows = generator(k, m)
-    parts = [(y0, min(m, y0 + ROWS_PER_PART)) for y0 in range(0, m, ROWS_PER_PART)]
+    P, CW, R, minw = shape(k, m)
+    per = (m + P - 1) // P
+    parts = [(y0, min(m, y0 + per)) for y0 in range(0, m, per)]
     name = f"k{k}_m{m}"
     out = [f"// GENERATED by tools/gen_fixed_kernels.py -- do not edit. (k={k}, m={m})",
            "// Compile-time-scheduled windowed bitmatrix product for one generator; see the",
            "// generator's docstring and DESIGN.md.",
+           "#pragma once",
            '#include "../fixed_common.hpp"',
            "",
            "namespace sh {",
            "namespace fixed {",
            ""]
     for p, (y0, y1) in enumerate(parts):
-        body = Body(k, rows, y0, y1).emit()
+        body = Body(k, rows, y0, y1).emit(R)
         nr = y1 - y0
         out.append(f"template <class Src>")
         out.append(f"__device__ __forceinline__ void run_{name}_p{p}(const Src &src, const Sink &sink) {{")
@@ -190,10 +223,10 @@ def gen_config(k, m):
         out.append(f"    for (int y = 0; y < {nr}; ++y) for (int b = 0; b < 8; ++b) ZERO(acc[y][b]);")
         out.append(body)
         out.append("    __builtin_amdgcn_sched_barrier(0);")
-        out.append(f"    // epilogue: (decode) + received recovery row, then store rows {y0}..{y1 - 1}")
+        out.append(f"    // epilogue: (decode) + received recovery rows, end fix-up, store rows {y0}..{y1 - 1}")
+        out.append(f"    src.template epilogue<{y0}, {nr}>(acc);")
         for yi in range(nr):
             out.append("    __builtin_amdgcn_sched_barrier(0);")
-            out.append(f"    src.add_row({y0 + yi}, acc[{yi}]);")
             for b in range(8):
                 out.append(f"    sink.store({y0 + yi}, {b}, acc[{yi}][{b}]);")
         out.append("}")
@@ -206,12 +239,21 @@ def gen_config(k, m):
     out.append("}")
     out.append("}  // namespace fixed")
     out.append("}  // namespace sh")
-    out.append(f"FIXED_KERNELS({name}, {k}, {m}, {len(parts)}, {ROWS_PER_PART})")
     os.makedirs(OUTDIR, exist_ok=True)
-    path = os.path.join(OUTDIR, f"fixed_{name}.hip")
-    with open(path, "w") as f:
+    inc = os.path.join(OUTDIR, f"fixed_{name}.inc")
+    with open(inc, "w") as f:
         f.write("\n".join(out) + "\n")
-    return path
+    # One translation unit per kernel (encode / decode stage A): each is a ~30K-instruction
+    # straight-line function, so the build compiles them in parallel.
+    paths = []
+    for mode, dec in (("enc", "false"), ("dec", "true")):
+        path = os.path.join(OUTDIR, f"fixed_{name}_{mode}.hip")
+        with open(path, "w") as f:
+            f.write(f"// GENERATED by tools/gen_fixed_kernels.py -- do not edit. (k={k}, m={m}, {mode})\n"
+                    f'#include "fixed_{name}.inc"\n'
+                    f"FIXED_KERNEL({name}, {k}, {m}, {P}, {CW}, {R}, {minw}, {mode}, {dec})\n")
+        paths.append(path)
+    return paths
 
 
 # Snippet table for runtime coefficients (decode stage B, csrc/stageb.hip): snippet c computes
@@ -249,7 +291,7 @@ def main(argv=()):
     cfgs = CONFIGS
     if argv:
         cfgs = [tuple(map(int, a.split(","))) for a in argv]
-    paths = [gen_config(k, m) for (k, m) in cfgs]
+    paths = [p for (k, m) in cfgs for p in gen_config(k, m)]
     gen_snippets()
     # registry of generated shapes
     reg = ["// GENERATED by tools/gen_fixed_kernels.py -- list of compile-time-scheduled (k, m).",
