@@ -260,6 +260,7 @@ hipError_t launch_stage_b(Context &, const DecodeWS &w, int n_in, int B, int gro
     sh::StageBArgs b{};
     b.in = w.residual;
     b.in_gstride = static_cast<long long>(n_in) * B;
+    b.in_slack = 256;  // carve(): the residual carries 256 bytes of slack
     b.n_in = n_in;
     b.out = dst;
     b.out_gstride = static_cast<long long>(w.emax) * B;

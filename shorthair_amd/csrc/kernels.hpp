@@ -87,6 +87,7 @@ struct ScatterArgs {
 struct StageBArgs {
     const uint8_t *in;        // [G][n_in][B] residual rows (>= 4 readable slack bytes at the end)
     long long in_gstride;
+    long long in_slack;       // readable bytes past groups * in_gstride
     int n_in;
     uint8_t *out;             // [G][emax][B]
     long long out_gstride;

@@ -21,6 +21,8 @@
 #include "kernels.hpp"
 #include "snippets.h"
 
+#include <algorithm>
+
 namespace sh {
 
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
@@ -125,8 +127,145 @@ __global__ __launch_bounds__(256) void stageb_snip(StageBArgs a) {
     }
 }
 
+// LDS-staged variant (the fixed-generator decode path: n_in <= 32, nq % 4 == 0, sub >= 16). One
+// workgroup = one group x one 64-column chunk x 32 outputs (4 waves x 8). The group's residual
+// rows for the chunk (n_in x 8 sub-blocks x ncols words, <= 64 KB) are gathered into LDS by
+// LDS-DMA up front, so the loop over input rows reads LDS (the next row prefetched into
+// registers under the current row's snippet calls) instead of waiting on HBM once per row.
+// Columns follow the fixed kernels' layout: the last 4-column chunk of each sub-block is
+// shifted back to end at the sub-block's end (fixed_common.hpp), so loads and stores are whole
+// dwords with no tail handling.
+__device__ __forceinline__ uint32_t colx_off(int q, int nq, int sub) {
+    return 4u * q - (q >= nq - 4 ? static_cast<uint32_t>(4 * nq - sub) : 0u);
+}
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+__global__ __launch_bounds__(256, 3) void stageb_lds(StageBArgs a) {
+    SH_SNIPPET_TABLE(L);
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const Geometry geo = a.geo;
+    const int ncc = (geo.nq + 63) / 64;
+    const int g = blockIdx.x / ncc;
+    const int cc = blockIdx.x - g * ncc;
+    const int c0 = cc * 64;
+    const int ncols = min(64, geo.nq - c0);
+    const int nch = ncols / 4;        // 16-byte chunks per (row, sub-block)
+    const int cpb = nch * 16;         // LDS bytes per (row, sub-block)
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int e = a.e[g];
+    const int j0 = (blockIdx.y * 4 + wave) * 8;
+
+    // ---- gather the residual tile into LDS: chunk ch = (y*8 + a)*nch + t
+    {
+        const long long gbase = static_cast<long long>(g) * a.in_gstride;
+        long long avail = static_cast<long long>(a.groups) * a.in_gstride + a.in_slack - gbase;
+        if (avail > 0x7FFFFFFFll) avail = 0x7FFFFFFFll;
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t *>(a.in + gbase), static_cast<short>(0), static_cast<int>(avail), 0x00020000);
+        const int total = a.n_in * 8 * nch;
+        for (int base = wave * 64; base < total; base += 256) {  // uniform
+            const int ch = base + lane;
+            uint32_t off = 0x80000000u;
+            if (ch < total) {
+                const int ya = ch / nch, t = ch - ya * nch;
+                const int y = ya >> 3, sa = ya & 7;
+                off = static_cast<uint32_t>(y) * geo.B + static_cast<uint32_t>(sa) * geo.sub +
+                      colx_off(c0 + 4 * t, geo.nq, geo.sub);
+            }
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t *)(lds + base * 16), 16, off, 0, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    if (j0 >= e) return;  // wave-uniform (after the barrier)
+
+    uint64_t snip;
+    asm volatile(
+        "s_getpc_b64 s[42:43]\n"
+        "s_add_u32 s42, s42, sh_snip_baseL@rel32@lo+4\n"
+        "s_addc_u32 s43, s43, sh_snip_baseL@rel32@hi+12\n"
+        "s_mov_b64 %0, s[42:43]"
+        : "=s"(snip)
+        :
+        : "s42", "s43", "scc");
+
+    const uint8_t *coef = a.coefT + static_cast<long long>(g) * a.coefT_gstride + j0;
+    const uint8_t *rd = lds + 4 * lane;
+
+    uint32_t acc[8][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[j][b] = 0;
+
+    uint32_t d[8], dn[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) d[s] = *reinterpret_cast<const uint32_t *>(rd + s * cpb);
+    for (int y = 0; y < a.n_in; ++y) {
+        // prefetch the next row (the LDS tile is padded by one row of zeros' worth of reads)
+        const int yn = y + 1 < a.n_in ? y + 1 : y;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) dn[s] = *reinterpret_cast<const uint32_t *>(rd + (yn * 8 + s) * cpb);
+        const uint64_t cw = *reinterpret_cast<const uint64_t *>(coef + static_cast<long long>(y) * a.ldT);
+        if (cw != 0) {  // wave-uniform: no output of this wave uses input y otherwise
+            u32x16 t0, t1;
+            t0[0] = 0;
+            t1[0] = 0;
+            t0[1] = d[0]; t0[2] = d[1]; t0[4] = d[2]; t0[8] = d[3];
+            t1[1] = d[4]; t1[2] = d[5]; t1[4] = d[6]; t1[8] = d[7];
+            t0[3] = t0[1] ^ t0[2]; t0[5] = t0[1] ^ t0[4]; t0[6] = t0[2] ^ t0[4]; t0[7] = t0[3] ^ t0[4];
+            t0[9] = t0[1] ^ t0[8]; t0[10] = t0[2] ^ t0[8]; t0[11] = t0[3] ^ t0[8]; t0[12] = t0[4] ^ t0[8];
+            t0[13] = t0[5] ^ t0[8]; t0[14] = t0[6] ^ t0[8]; t0[15] = t0[7] ^ t0[8];
+            t1[3] = t1[1] ^ t1[2]; t1[5] = t1[1] ^ t1[4]; t1[6] = t1[2] ^ t1[4]; t1[7] = t1[3] ^ t1[4];
+            t1[9] = t1[1] ^ t1[8]; t1[10] = t1[2] ^ t1[8]; t1[11] = t1[3] ^ t1[8]; t1[12] = t1[4] ^ t1[8];
+            t1[13] = t1[5] ^ t1[8]; t1[14] = t1[6] ^ t1[8]; t1[15] = t1[7] ^ t1[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t c = static_cast<uint32_t>(cw >> (8 * j)) & 0xffu;
+                if (c == 0) continue;  // wave-uniform
+                u32x8 tmp;
+                SH_SNIP_CALL(snip + (static_cast<uint64_t>(c) << 6), t0, t1, tmp);
+#pragma unroll
+                for (int b = 0; b < 8; ++b) acc[j][b] ^= tmp[b];
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) d[s] = dn[s];
+    }
+
+    if (lane >= ncols) return;
+    const uint32_t col = colx_off(c0 + lane, geo.nq, geo.sub);
+    uint8_t *out = a.out + static_cast<long long>(g) * a.out_gstride + col;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (j0 + j >= e) break;
+        uint8_t *row = out + static_cast<long long>(j0 + j) * geo.B;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const uint32_t w = acc[j][b];
+            __builtin_memcpy(row + b * geo.sub, &w, 4);
+        }
+    }
+}
+
+bool stageb_lds_ok(const StageBArgs &a) {
+    return a.n_in <= 32 && a.geo.nq % 4 == 0 && a.geo.sub >= 16;
+}
+
 hipError_t launch_stageb(const StageBArgs &a, int emax, hipStream_t stream) {
     if (a.groups <= 0 || emax <= 0) return hipSuccess;
+    if (stageb_lds_ok(a)) {
+        const int ncc = (a.geo.nq + 63) / 64;
+        const int nch = std::min(64, a.geo.nq) / 4;
+        // tile bytes rounded up to whole 4-wave DMA rounds (out-of-range lanes still write LDS)
+        const size_t chunks = static_cast<size_t>(a.n_in) * 8 * nch;
+        const size_t lds = ((chunks + 255) / 256) * 256 * 16;
+        dim3 grid(static_cast<unsigned>(ncc) * a.groups, (emax + 31) / 32, 1);
+        hipLaunchKernelGGL(stageb_lds, grid, dim3(256), lds, stream, a);
+        return hipGetLastError();
+    }
     dim3 grid(static_cast<unsigned>((a.geo.nq + 63) / 64) * a.groups, (emax + 31) / 32, 1);
     hipLaunchKernelGGL(stageb_snip, grid, dim3(256), 0, stream, a);
     return hipGetLastError();
