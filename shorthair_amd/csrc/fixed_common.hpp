@@ -54,7 +54,13 @@ namespace fixed {
 // 2-input XOR as a bitop3 (third operand ignored): opaque to LLVM's reassociation.
 #define X2(a, b) __builtin_amdgcn_bitop3_b32((a), (b), (a), 0x3C)
 
+// Cache policy of the output stores (aux operand of the buffer store).
+#ifndef SH_STORE_AUX
+#define SH_STORE_AUX 0
+#endif
+
 typedef __attribute__((address_space(3))) void lds_void;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t OOR = 0x80000000u;  // buffer offset past every descriptor's range (< 2 GiB)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const uint8_t *p, uint32_t bytes) {
@@ -169,6 +175,9 @@ struct Src {
 
     // DMA of input step x into its ring slot.
     __device__ __forceinline__ void issue(int x, const Pre &pr) const {
+#ifdef SH_EXPERIMENT_NO_DMA  // timing experiment only: compute on whatever the ring holds
+        return;
+#endif
         uint8_t *slot = const_cast<uint8_t *>(lds) + (x % S::R) * S::SLOT;
 #pragma unroll
         for (int j = 0; j < S::DPW; ++j) {
@@ -224,25 +233,51 @@ struct Src {
     }
 };
 
-// Output: one dword store per word (the shifted last chunk makes every word a full real one);
-// lanes past the last group get an out-of-range offset, dropped by the buffer unit.
+// Output, transposed through a per-wave 2 KB LDS scratch so every store is 16 contiguous bytes:
+// a lane holds word q of the 8 sub-blocks of a row; it writes them to scratch[b][lane], then
+// reads back two 16-byte items (sub-block b, 4-column chunk t) and stores each with one
+// buffer_store_dwordx4 -- 2 store instructions per row instead of 8 dword stores. A chunk lies
+// in one group (nq % 4 == 0) and is contiguous in memory (the shifted last chunk included).
+// Item i = lane + 64h (h = 0, 1): b = i / 16, t = i % 16. Chunks past the last group get an
+// out-of-range offset, dropped by the buffer unit.
 struct Sink {
     __amdgpu_buffer_rsrc_t rsrc;
-    uint32_t voff, B, sub;
-    __device__ __forceinline__ void init(const FixedArgs &a, const WGInfo &w) {
+    uint32_t voff[2];         // per item: chunk base + b * sub (or OOR)
+    uint32_t B;
+    uint8_t *scr;             // this wave's scratch [8][64] words
+    int lane;
+    __device__ __forceinline__ void init(const FixedArgs &a, const WGInfo &w, uint8_t *scratch) {
         const Geometry &geo = a.geo;
         rsrc = wg_rsrc(a.out, a.out_bytes, a.out_gstride, w.g_first);
         B = geo.B;
-        sub = geo.sub;
-        voff = w.valid ? static_cast<uint32_t>(w.gl) * static_cast<uint32_t>(a.out_gstride) + col_off(w.q, geo)
-                       : OOR;
+        lane = w.lane;
+        scr = scratch;
+        const int t = w.lane & 15;
+        const long long colx = w.col0 + (w.c - w.lane) + 4 * t;  // first column of chunk t
+        const int gx = static_cast<int>(colx / geo.nq);
+        const int qx = static_cast<int>(colx - static_cast<long long>(gx) * geo.nq);
+        const uint32_t base = static_cast<uint32_t>(gx - w.g_first) * static_cast<uint32_t>(a.out_gstride) +
+                              col_off(qx, geo);
+        const bool ok = gx < a.groups;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int b = (w.lane >> 4) + 4 * h;
+            voff[h] = ok ? base + static_cast<uint32_t>(b) * geo.sub : OOR;
+        }
     }
-    __device__ __forceinline__ void store(int y, int b, uint32_t w) const {
-#ifdef SH_EXPERIMENT_NO_STORE  // timing experiment only: keep the value, drop the store
-        asm volatile("" ::"v"(w));
+    __device__ __forceinline__ void store_row(int y, const uint32_t (&w)[8]) const {
+#ifdef SH_EXPERIMENT_NO_STORE  // timing experiment only: keep the values, drop the stores
+        asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]), "v"(w[6]), "v"(w[7]));
         return;
 #endif
-        __builtin_amdgcn_raw_buffer_store_b32(w, rsrc, voff, static_cast<uint32_t>(y) * B + static_cast<uint32_t>(b) * sub, 0);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) reinterpret_cast<uint32_t *>(scr)[b * 64 + lane] = w[b];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int i = lane + 64 * h;
+            const u32x4 v = *reinterpret_cast<const u32x4 *>(scr + (i >> 4) * 256 + (i & 15) * 16);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, voff[h], static_cast<uint32_t>(y) * B, SH_STORE_AUX);
+        }
     }
 };
 
@@ -267,7 +302,7 @@ __device__ __forceinline__ int kernel_prologue(const FixedArgs &a, uint8_t *lds,
     w.q = static_cast<int>(col - static_cast<long long>(g) * nq);
     w.gl = g - w.g_first;
     w.valid = g < a.groups;
-    uint8_t *lds_pos = lds + S::R * S::SLOT;
+    uint8_t *lds_pos = lds + S::R * S::SLOT + S::NW * 2048;
     if (DEC) {
         const int ng = a.groups_per_wg;
         constexpr int TW = (S::KP + S::MP) / 4;
@@ -285,7 +320,7 @@ __device__ __forceinline__ int kernel_prologue(const FixedArgs &a, uint8_t *lds,
         __syncthreads();
     }
     src.init(a, w, lds, lds_pos);
-    sink.init(a, w);
+    sink.init(a, w, lds + S::R * S::SLOT + w.wave * 2048);
 #pragma unroll
     for (int x = 0; x < S::R - 1 && x < S::K; ++x) src.issue(x, src.pre(x));
     return part;
@@ -296,7 +331,7 @@ inline hipError_t launch_shape(FixedArgs a, bool dec, hipStream_t s, void (*kern
     a.groups_per_wg = (S::COLS - 1) / a.geo.nq + 2;
     const long long cols = static_cast<long long>(a.groups) * a.geo.nq;
     const unsigned blocks = static_cast<unsigned>((cols + S::COLS - 1) / S::COLS);
-    const size_t lds = static_cast<size_t>(S::R) * S::SLOT +
+    const size_t lds = static_cast<size_t>(S::R) * S::SLOT + S::NW * 2048 +  // ring + store scratch
                        (dec ? static_cast<size_t>(a.groups_per_wg) * (S::KP + S::MP) : 0);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(S::NT), lds, s, a);
     return hipGetLastError();

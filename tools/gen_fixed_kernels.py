@@ -189,7 +189,7 @@ def shape(k, m):
     # lockstep (one barrier per step), so they share every instruction-cache line they fetch.
     # (With one wave per part the code stream -- ~0.7 KB per step and part -- outweighs the data
     # stream and instruction fetch, not HBM, bounds the kernel.)
-    CW = int(os.environ.get("SH_CW", str(max(1, min(8, 16 // P)))))
+    CW = int(os.environ.get("SH_CW", str(max(1, min(8, 8 // P)))))
     slot = 8 * CW * 64 * 4
     R = int(os.environ.get("SH_RING", str(max(3, min(8, 65536 // slot)))))
     rows = (m + P - 1) // P
@@ -227,8 +227,7 @@ def gen_config(k, m):
         out.append(f"    src.template epilogue<{y0}, {nr}>(acc);")
         for yi in range(nr):
             out.append("    __builtin_amdgcn_sched_barrier(0);")
-            for b in range(8):
-                out.append(f"    sink.store({y0 + yi}, {b}, acc[{yi}][{b}]);")
+            out.append(f"    sink.store_row({y0 + yi}, acc[{yi}]);")
         out.append("}")
         out.append("")
     out.append(f"template <class Src>")
