@@ -53,6 +53,9 @@ namespace fixed {
 #define ZERO(r) asm volatile("v_mov_b32 %0, 0" : "=v"(r))
 // 2-input XOR as a bitop3 (third operand ignored): opaque to LLVM's reassociation.
 #define X2(a, b) __builtin_amdgcn_bitop3_b32((a), (b), (a), 0x3C)
+// acc ^= t as a 4-byte VOP2 v_xor_b32 (half the bytes of a bitop3: the straight-line schedules
+// are instruction-fetch heavy); a non-volatile asm is opaque to reassociation yet schedulable.
+#define XV(acc, t) asm("v_xor_b32 %0, %1, %2" : "=v"(acc) : "v"(t), "v"(acc))
 
 // Cache policy of the output stores (aux operand of the buffer store).
 #ifndef SH_STORE_AUX

@@ -112,14 +112,14 @@ class Body:
         if name in have:
             return name
         bits = [b for b in (1, 2, 4, 8) if v & b]
-        if len(bits) == 2:
-            self.lines.append(f"    const uint32_t {name} = X2({base[bits[0]]}, {base[bits[1]]});")
+        if len(bits) == 2:  # plain XOR: 4-byte VOP2 encoding (code size is fetch bandwidth)
+            self.lines.append(f"    const uint32_t {name} = {base[bits[0]]} ^ {base[bits[1]]};")
         elif len(bits) == 3:
             self.lines.append(f"    const uint32_t {name} = X3({base[bits[0]]}, {base[bits[1]]}, {base[bits[2]]});")
         else:  # 15 = 3 ^ 12
             a = self.table_expr(h, 3, have, d)
             b = self.table_expr(h, 12, have, d)
-            self.lines.append(f"    const uint32_t {name} = X2({a}, {b});")
+            self.lines.append(f"    const uint32_t {name} = {a} ^ {b};")
         have.add(name)
         return name
 
@@ -168,9 +168,9 @@ class Body:
                     tb = self.table_expr(1, hi, have, cur)
                     L.append(f"    {acc} = X3({acc}, {ta}, {tb});")
                 elif lo:
-                    L.append(f"    {acc} = X2({acc}, {self.table_expr(0, lo, have, cur)});")
+                    L.append(f"    XV({acc}, {self.table_expr(0, lo, have, cur)});")
                 else:
-                    L.append(f"    {acc} = X2({acc}, {self.table_expr(1, hi, have, cur)});")
+                    L.append(f"    XV({acc}, {self.table_expr(1, hi, have, cur)});")
             # Tie every accumulator to this step (an empty volatile asm is a chained side effect):
             # otherwise the DAG scheduler floats the pure bitop3 nodes of a ~30K-node basic block
             # away from their loads and keeps every loaded word live.
