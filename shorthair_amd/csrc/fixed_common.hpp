@@ -284,6 +284,19 @@ struct Sink {
     }
 };
 
+// XCD-aware tile order. Workgroups are dealt round-robin over the 8 XCDs (block b -> XCD b % 8;
+// a speed assumption, never a correctness one). Adjacent column tiles usually split a group, so
+// both read the same 128-byte lines at their shared edge; giving them blocks b and b + 8 puts
+// them on one XCD at about the same time, and the second read hits that XCD's L2 instead of
+// going to HBM again (measured: 29% over-fetch on the staging microbenchmark without it).
+// Bijective map of block b in [0, n) to a tile: XCD i gets the contiguous tile range
+// [start_i, start_i + count_i), count_i = n/8 (+1 for the first n%8 XCDs).
+__device__ __forceinline__ int xcd_tile(int b, int n) {
+    const int q = n >> 3, r = n & 7;
+    const int x = b & 7, i = b >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
 // Sets up src/sink, issues the ring's first R-1 DMAs and returns this wave's part. The caller
 // (the FIXED_KERNEL macro) then calls the generated run_<name> directly, so everything inlines
 // into one function: a non-inlined body took `src` by reference through scratch and read the
@@ -297,7 +310,7 @@ __device__ __forceinline__ int kernel_prologue(const FixedArgs &a, uint8_t *lds,
     const int part = w.wave % S::P;
     const int cw = w.wave / S::P;
     w.c = cw * 64 + w.lane;
-    w.col0 = static_cast<long long>(blockIdx.x) * S::COLS;
+    w.col0 = static_cast<long long>(xcd_tile(blockIdx.x, gridDim.x)) * S::COLS;
     const int nq = a.geo.nq;
     w.g_first = static_cast<int>(w.col0 / nq);
     const long long col = w.col0 + w.c;
