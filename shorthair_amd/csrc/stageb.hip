@@ -157,14 +157,17 @@ __global__ __launch_bounds__(256, 3) void stageb_lds(StageBArgs a) {
     const int e = a.e[g];
     const int j0 = (blockIdx.y * 4 + wave) * 8;
 
-    // ---- gather the residual tile into LDS: chunk ch = (y*8 + a)*nch + t
+    // ---- gather the residual tile into LDS: chunk ch = (y*8 + a)*nch + t; then the group's
+    // stage-B coefficients (n_in x ldT bytes) behind it
+    const int total = a.n_in * 8 * nch;
+    const int tile = ((total + 255) / 256) * 256 * 16;
+    uint8_t *lcoef = lds + tile;
     {
         const long long gbase = static_cast<long long>(g) * a.in_gstride;
         long long avail = static_cast<long long>(a.groups) * a.in_gstride + a.in_slack - gbase;
         if (avail > 0x7FFFFFFFll) avail = 0x7FFFFFFFll;
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<uint8_t *>(a.in + gbase), static_cast<short>(0), static_cast<int>(avail), 0x00020000);
-        const int total = a.n_in * 8 * nch;
         for (int base = wave * 64; base < total; base += 256) {  // uniform
             const int ch = base + lane;
             uint32_t off = 0x80000000u;
@@ -176,6 +179,12 @@ __global__ __launch_bounds__(256, 3) void stageb_lds(StageBArgs a) {
             }
             __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t *)(lds + base * 16), 16, off, 0, 0, 0);
         }
+        const int cbytes = a.n_in * a.ldT;  // multiple of 8; <= 32 * 32
+        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t *>(a.coefT + static_cast<long long>(g) * a.coefT_gstride), static_cast<short>(0),
+            cbytes, 0x00020000);
+        for (int base = wave * 64; base * 16 < cbytes; base += 256)  // uniform
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rc, (lds_void_t *)(lcoef + base * 16), 16, (base + lane) * 16, 0, 0, 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
@@ -191,8 +200,8 @@ __global__ __launch_bounds__(256, 3) void stageb_lds(StageBArgs a) {
         :
         : "s42", "s43", "scc");
 
-    const uint8_t *coef = a.coefT + static_cast<long long>(g) * a.coefT_gstride + j0;
     const uint8_t *rd = lds + 4 * lane;
+    const uint8_t *cf = lcoef + j0;
 
     uint32_t acc[8][8];
 #pragma unroll
@@ -200,16 +209,18 @@ __global__ __launch_bounds__(256, 3) void stageb_lds(StageBArgs a) {
 #pragma unroll
         for (int b = 0; b < 8; ++b) acc[j][b] = 0;
 
+    // rows and coefficients are prefetched one input row ahead (LDS latency under the calls)
     uint32_t d[8], dn[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) d[s] = *reinterpret_cast<const uint32_t *>(rd + s * cpb);
+    uint2 cv = *reinterpret_cast<const uint2 *>(cf);
     for (int y = 0; y < a.n_in; ++y) {
-        // prefetch the next row (the LDS tile is padded by one row of zeros' worth of reads)
         const int yn = y + 1 < a.n_in ? y + 1 : y;
 #pragma unroll
         for (int s = 0; s < 8; ++s) dn[s] = *reinterpret_cast<const uint32_t *>(rd + (yn * 8 + s) * cpb);
-        const uint64_t cw = *reinterpret_cast<const uint64_t *>(coef + static_cast<long long>(y) * a.ldT);
-        if (cw != 0) {  // wave-uniform: no output of this wave uses input y otherwise
+        const uint2 cvn = *reinterpret_cast<const uint2 *>(cf + yn * a.ldT);
+        const uint32_t clo = __builtin_amdgcn_readfirstlane(cv.x), chi = __builtin_amdgcn_readfirstlane(cv.y);
+        if ((clo | chi) != 0) {  // wave-uniform: no output of this wave uses input y otherwise
             u32x16 t0, t1;
             t0[0] = 0;
             t1[0] = 0;
@@ -223,8 +234,9 @@ __global__ __launch_bounds__(256, 3) void stageb_lds(StageBArgs a) {
             t1[13] = t1[5] ^ t1[8]; t1[14] = t1[6] ^ t1[8]; t1[15] = t1[7] ^ t1[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const uint32_t c = static_cast<uint32_t>(cw >> (8 * j)) & 0xffu;
-                if (c == 0) continue;  // wave-uniform
+                // dense S^-1 (every coefficient of a received row is nonzero for e = m): no per-j
+                // skip; a zero coefficient simply runs snippet 0 (adds nothing)
+                const uint32_t c = ((j < 4 ? clo : chi) >> (8 * (j & 3))) & 0xffu;
                 u32x8 tmp;
                 SH_SNIP_CALL(snip + (static_cast<uint64_t>(c) << 6), t0, t1, tmp);
 #pragma unroll
@@ -233,6 +245,7 @@ __global__ __launch_bounds__(256, 3) void stageb_lds(StageBArgs a) {
         }
 #pragma unroll
         for (int s = 0; s < 8; ++s) d[s] = dn[s];
+        cv = cvn;
     }
 
     if (lane >= ncols) return;
@@ -251,7 +264,7 @@ __global__ __launch_bounds__(256, 3) void stageb_lds(StageBArgs a) {
 }
 
 bool stageb_lds_ok(const StageBArgs &a) {
-    return a.n_in <= 32 && a.geo.nq % 4 == 0 && a.geo.sub >= 16;
+    return a.n_in <= 32 && a.ldT <= 32 && a.geo.nq % 4 == 0 && a.geo.sub >= 16;
 }
 
 hipError_t launch_stageb(const StageBArgs &a, int emax, hipStream_t stream) {
@@ -261,7 +274,8 @@ hipError_t launch_stageb(const StageBArgs &a, int emax, hipStream_t stream) {
         const int nch = std::min(64, a.geo.nq) / 4;
         // tile bytes rounded up to whole 4-wave DMA rounds (out-of-range lanes still write LDS)
         const size_t chunks = static_cast<size_t>(a.n_in) * 8 * nch;
-        const size_t lds = ((chunks + 255) / 256) * 256 * 16;
+        const size_t cbytes = static_cast<size_t>(a.n_in) * a.ldT;  // coefficients behind the tile
+        const size_t lds = ((chunks + 255) / 256) * 256 * 16 + ((cbytes + 4095) / 4096) * 4096;
         dim3 grid(static_cast<unsigned>(ncc) * a.groups, (emax + 31) / 32, 1);
         hipLaunchKernelGGL(stageb_lds, grid, dim3(256), lds, stream, a);
         return hipGetLastError();
