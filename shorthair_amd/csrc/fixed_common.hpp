@@ -122,8 +122,6 @@ struct Src {
     uint32_t B, sub;
     int wave;
     uint32_t rd;              // this lane's read offset in a slot (c * 4)
-    uint32_t lbase;           // decode epilogue: gl * gstride + col_off(q)
-    int gl;
     const uint8_t *lds;       // ring base
     const uint8_t *pos;       // decode: [groups_per_wg][KP + MP] position tables (LDS)
 
@@ -138,8 +136,6 @@ struct Src {
         wave = w.wave;
         rd = static_cast<uint32_t>(w.c) * 4u;
         const uint32_t gstride = static_cast<uint32_t>(a.in_gstride);
-        gl = w.gl;
-        lbase = static_cast<uint32_t>(w.gl) * gstride + col_off(w.q, geo);
 #pragma unroll
         for (int j = 0; j < S::DPW; ++j) {
             const int off = (w.wave * S::DPW + j) * 64 * S::W + w.lane * S::W;
@@ -212,26 +208,57 @@ struct Src {
     }
 
     // Epilogue for output rows Y0..Y0+NR-1 of this part (decode only): acc ^= the received
-    // recovery block of generator row y (zeros when absent); all loads of a batch of rows are
-    // issued before the first XOR (one memory round trip per batch).
+    // recovery block of generator row y (zeros when absent). Loaded as 16-byte items (sub-block
+    // b, 4-column chunk t; item i = lane + 64h: b = i / 16, t = i % 16, the store layout of Sink)
+    // with buffer_load_dwordx4 and transposed back to one word per lane through the wave's LDS
+    // scratch: 2 load instructions per row instead of 8, all loads of 4 rows in flight together.
+    uint32_t cbase[2];        // decode epilogue: item chunk base (block 0 of the chunk's group)
+    int cgl;                  // decode epilogue: the item chunk's group (position-table index)
+    uint8_t *scr;             // this wave's LDS scratch [8][64] words
+    int lane;
+
+    __device__ __forceinline__ void init_items(const FixedArgs &a, const WGInfo &w, uint8_t *scratch) {
+        const Geometry &geo = a.geo;
+        scr = scratch;
+        lane = w.lane;
+        const int t = w.lane & 15;
+        const long long colx = w.col0 + (w.c - w.lane) + 4 * t;
+        const int gx = static_cast<int>(colx / geo.nq);
+        const int qx = static_cast<int>(colx - static_cast<long long>(gx) * geo.nq);
+        cgl = gx - w.g_first;
+        const uint32_t base = static_cast<uint32_t>(cgl) * static_cast<uint32_t>(a.in_gstride) + col_off(qx, geo);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            cbase[h] = gx < a.groups ? base + static_cast<uint32_t>((w.lane >> 4) + 4 * h) * geo.sub : OOR;
+    }
+
     template <int Y0, int NR>
     __device__ __forceinline__ void epilogue(uint32_t (&acc)[NR][8]) const {
         if (!DEC) return;
-        constexpr int CH = 4;  // rows per batch of loads (register budget)
+        constexpr int CH = 4;  // rows per batch of loads (register budget: 8 x 4 VGPRs)
 #pragma unroll
         for (int y0 = 0; y0 < NR; y0 += CH) {
-            uint32_t v[CH][8];
+            u32x4 v[CH][2];
 #pragma unroll
             for (int yi = 0; yi < CH && y0 + yi < NR; ++yi) {
-                const int p = pos[gl * (S::KP + S::MP) + S::KP + Y0 + y0 + yi];
-                const uint32_t o = p == 0xFF ? OOR : lbase + static_cast<uint32_t>(p) * B;
+                const int p = pos[cgl * (S::KP + S::MP) + S::KP + Y0 + y0 + yi];
 #pragma unroll
-                for (int aa = 0; aa < 8; ++aa) v[yi][aa] = bload(rsrc, o, aa * sub);
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t o = (p == 0xFF || cbase[h] == OOR) ? OOR : cbase[h] + static_cast<uint32_t>(p) * B;
+                    v[yi][h] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, 0, 0);
+                }
             }
 #pragma unroll
-            for (int yi = 0; yi < CH && y0 + yi < NR; ++yi)
+            for (int yi = 0; yi < CH && y0 + yi < NR; ++yi) {
 #pragma unroll
-                for (int aa = 0; aa < 8; ++aa) acc[y0 + yi][aa] = X2(acc[y0 + yi][aa], v[yi][aa]);
+                for (int h = 0; h < 2; ++h) {
+                    const int i = lane + 64 * h;
+                    *reinterpret_cast<u32x4 *>(scr + (i >> 4) * 256 + (i & 15) * 16) = v[yi][h];
+                }
+#pragma unroll
+                for (int aa = 0; aa < 8; ++aa)
+                    acc[y0 + yi][aa] = X2(acc[y0 + yi][aa], reinterpret_cast<const uint32_t *>(scr)[aa * 64 + lane]);
+            }
         }
     }
 };
@@ -336,6 +363,7 @@ __device__ __forceinline__ int kernel_prologue(const FixedArgs &a, uint8_t *lds,
         __syncthreads();
     }
     src.init(a, w, lds, lds_pos);
+    if (DEC) src.init_items(a, w, lds + S::R * S::SLOT + w.wave * 2048);
     sink.init(a, w, lds + S::R * S::SLOT + w.wave * 2048);
 #pragma unroll
     for (int x = 0; x < S::R - 1 && x < S::K; ++x) src.issue(x, src.pre(x));
