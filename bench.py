@@ -9,9 +9,12 @@ sharded with no data-path collective (independent units -> weak scaling); timing
 barrier + synchronize and the max over ranks is reported.
 
 value = algorithmic GiB/s over all ranks: encode moves (k+m)*B and decode (k+e)*B bytes per group
-(SURVEY.md §8d). roofline: the dominant op, timed with HIP events on the stream its kernels run
-on, against the 8 TB/s HBM3E peak. cpu_baseline: the reference codec (oracle/_ref, compiled from
-catid/shorthair) on the host cores, rank 0 only, bounded sample.
+(SURVEY.md §8d). roofline: the dominant kernel -- the encode kernel (the whole encode op is one
+launch; bench's HIP events on the launch stream) or decode stage A (the library's own HIP
+events around that launch, cauchy_256_profile), whichever takes longer; both move (k+m)*B
+algorithmic bytes per group (read k blocks, write m rows) -- against the 8 TB/s HBM3E peak.
+cpu_baseline: the reference codec (oracle/_ref, compiled from catid/shorthair) on the host cores,
+rank 0 only, bounded sample.
 """
 import argparse
 import json
@@ -166,6 +169,7 @@ def main():
 
     # ---- timed region ----
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    sh.profile(args.steps)  # decode stage events, recorded on the stream without host syncs
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -178,6 +182,8 @@ def main():
     elapsed = time.perf_counter() - t0
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    stages = sh.profile_read() or (float("nan"),) * 3
+    sh.profile(0)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -195,7 +201,9 @@ def main():
     if rank == 0:
         enc_bw = enc_bytes / (enc_ms * 1e-3)
         dec_bw = dec_bytes / (dec_ms * 1e-3)
-        dom = ("encode", enc_ms, enc_bw, enc_bytes) if enc_ms >= dec_ms else ("decode", dec_ms, dec_bw, dec_bytes)
+        kb = G * (k + m) * B  # algorithmic bytes per launch of either compile-time kernel
+        a_ms = stages[1]
+        dom = (("encode kernel", enc_ms) if not (a_ms > enc_ms) else ("decode stage-A kernel", a_ms))
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         cpu = None if args.no_cpu else cpu_baseline(k, m, B, args.erasures, args.cpu_seconds, threads)
         line = {
@@ -218,11 +226,13 @@ def main():
             "hbm_frac": round(value * 2**30 / world / HBM_PEAK, 4),
             "payload_GiBps": round(G * world * k * B * 2 * args.steps / elapsed / 2**30, 3),
             "ops": {"encode_ms": round(enc_ms, 4), "encode_GBps": round(enc_bw / 1e9, 1),
-                    "decode_ms": round(dec_ms, 4), "decode_GBps": round(dec_bw / 1e9, 1)},
-            "roofline": {"bound": "hbm", "kernel": dom[0], "achieved": round(dom[2] / 1e9, 1),
+                    "decode_ms": round(dec_ms, 4), "decode_GBps": round(dec_bw / 1e9, 1),
+                    "decode_setup_ms": round(stages[0], 4), "decode_stageA_ms": round(stages[1], 4),
+                    "decode_stageB_ms": round(stages[2], 4)},
+            "roofline": {"bound": "hbm", "kernel": dom[0], "achieved": round(kb / (dom[1] * 1e-3) / 1e9, 1),
                          "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                         "frac": round(dom[2] / HBM_PEAK, 4), "traffic": None,
-                         "alg_bytes_per_launch": dom[3]},
+                         "frac": round(kb / (dom[1] * 1e-3) / HBM_PEAK, 4), "traffic": None,
+                         "alg_bytes_per_launch": kb, "launch_ms": round(dom[1], 4)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

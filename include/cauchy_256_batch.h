@@ -59,6 +59,14 @@ int cauchy_256_fill_synthetic(void *d_out, int n, int block_bytes, int groups,
 void *cauchy_256_default_stream(void);
 int cauchy_256_sync(void *stream);
 
+/* Measurement hooks (bench.py's roofline): after cauchy_256_profile(n), each batched decode on
+ * the compile-time path records HIP events on its stream around its three kernels (the last n
+ * decodes are kept; nothing synchronises while recording; n = 0 turns it off).
+ * profile_read waits for them and returns ms[0..2] = mean setup, stage A and stage B times and
+ * the number of decodes averaged (-1: none recorded). */
+int cauchy_256_profile(int capacity);
+int cauchy_256_profile_read(float *ms);
+
 #ifdef __cplusplus
 }
 #endif

@@ -26,11 +26,11 @@ EXPORTED_SYMBOLS = [
     "_cauchy_256_init", "cauchy_256_encode", "cauchy_256_decode",
     "cauchy_256_batch_init", "cauchy_256_encode_batch", "cauchy_256_decode_batch",
     "cauchy_256_decode_batch_out", "cauchy_256_batch_reserve", "cauchy_256_fill_synthetic",
-    "cauchy_256_default_stream", "cauchy_256_sync",
+    "cauchy_256_default_stream", "cauchy_256_sync", "cauchy_256_profile", "cauchy_256_profile_read",
 ]
 
 if not os.path.exists(LIB_PATH):
-    raise ImportError(f"{LIB_PATH} not built: run `python -m shorthair_amd.build` "
+    raise ImportError(f"{LIB_PATH} not built: run `python shorthair_amd/build.py` "
                       "(the codec has no CPU fallback)")
 
 lib = ctypes.CDLL(LIB_PATH)
@@ -65,6 +65,10 @@ lib.cauchy_256_default_stream.argtypes = []
 lib.cauchy_256_default_stream.restype = _c.c_void_p
 lib.cauchy_256_sync.argtypes = [_c.c_void_p]
 lib.cauchy_256_sync.restype = _c.c_int
+lib.cauchy_256_profile.argtypes = [_c.c_int]
+lib.cauchy_256_profile.restype = _c.c_int
+lib.cauchy_256_profile_read.argtypes = [_c.c_void_p]
+lib.cauchy_256_profile_read.restype = _c.c_int
 
 
 class CodecError(RuntimeError):
@@ -142,3 +146,14 @@ def default_stream():
 
 def sync(stream=None):
     return _check(lib.cauchy_256_sync(stream), "sync")
+
+
+def profile(capacity=64):
+    """Record HIP events around the stages of the next `capacity` batched decodes (0: off)."""
+    return _check(lib.cauchy_256_profile(int(capacity)), "profile")
+
+
+def profile_read():
+    """Mean (setup_ms, stageA_ms, stageB_ms) over the recorded decodes, or None."""
+    ms = (ctypes.c_float * 3)()
+    return tuple(ms) if lib.cauchy_256_profile_read(ms) > 0 else None

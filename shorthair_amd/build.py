@@ -1,6 +1,6 @@
 """Build libcauchy256.so in-tree: hand-written HIP kernels for gfx950 + the C-ABI host library.
 
-    python -m shorthair_amd.build        (also run by __graft_entry__.build())
+    python shorthair_amd/build.py        (also run by __graft_entry__.build())
 
 hipcc cross-compiles for gfx950 without a GPU. The .so lands next to this file so it travels
 with the repository snapshot to the GPU box (it is git-ignored, not gpurun-ignored).

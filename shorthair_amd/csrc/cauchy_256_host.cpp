@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <algorithm>
 #include <cstring>
+#include <array>
 #include <map>
 #include <mutex>
 #include <utility>
@@ -85,6 +86,10 @@ struct Context {
     // decode setup.
     std::map<std::pair<int, int>, uint8_t *> gens;
     DevBuf ws;                        // decode workspace
+    // stage timing (cauchy_256_profile): per profiled decode, events around setup / stage A /
+    // stage B, in a ring of `evq.size()` quadruples (no host synchronisation while recording)
+    std::vector<std::array<hipEvent_t, 4>> evq;
+    int ev_next = 0, ev_count = 0;
     // single-group staging, guarded by stage_mu for the whole call
     std::mutex stage_mu;
     PinnedBuf h_stage;
@@ -301,7 +306,16 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
     sa.ldB = w.ldB;
     sa.pos = w.pos;
     sa.rpos = w.rpos;
+    hipEvent_t *ev = nullptr;
+    if (!c.evq.empty()) {
+        std::lock_guard<std::mutex> g(c.mu);
+        ev = c.evq[c.ev_next].data();
+        c.ev_next = (c.ev_next + 1) % static_cast<int>(c.evq.size());
+        c.ev_count = std::min(c.ev_count + 1, static_cast<int>(c.evq.size()));
+    }
+    if (ev) SH_CHECK(hipEventRecord(ev[0], s));
     SH_CHECK(sh::launch_decode_setup(sa, groups, s));
+    if (ev) SH_CHECK(hipEventRecord(ev[1], s));
 
     const Geometry geo = sh::make_geometry(B);
     if (w.fixed) {
@@ -309,8 +323,10 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
         //   residual_y = R_y + sum_{received x} M(C[y][x]) d_x
         SH_CHECK(launch_fixed_batch(k, m, B, groups, d_blocks, static_cast<long long>(k) * B,
                                       w.residual, static_cast<long long>(m) * B, w.pos, w.rpos, true, s));
+        if (ev) SH_CHECK(hipEventRecord(ev[2], s));
         // Stage B: recovered_j = sum_y M(S^-1[j][i(y)]) residual_y over the received rows y
         SH_CHECK(launch_stage_b(c, w, m, B, groups, dst, s));
+        if (ev) SH_CHECK(hipEventRecord(ev[3], s));
         return 0;
     }
     // Stage A: residual_i = R_i + sum_{orig j} M(C[r_i][row_j]) d_j  (per-group coefficients)
@@ -458,6 +474,37 @@ extern "C" void *cauchy_256_default_stream(void) {
     Context &c = ctx();
     if (ensure_init(c)) return nullptr;
     return c.stream;
+}
+
+extern "C" int cauchy_256_profile(int capacity) {
+    Context &c = ctx();
+    if (int rc = ensure_init(c)) return rc;
+    std::lock_guard<std::mutex> g(c.mu);
+    for (auto &q : c.evq)
+        for (hipEvent_t e : q) hipEventDestroy(e);
+    c.evq.assign(std::max(0, capacity), {});
+    for (auto &q : c.evq)
+        for (hipEvent_t &e : q) SH_CHECK(hipEventCreate(&e));
+    c.ev_next = c.ev_count = 0;
+    return 0;
+}
+
+extern "C" int cauchy_256_profile_read(float *ms) {
+    Context &c = ctx();
+    std::lock_guard<std::mutex> g(c.mu);
+    if (c.ev_count == 0) return -1;
+    double sum[3] = {0, 0, 0};
+    for (int i = 0; i < c.ev_count; ++i) {
+        const auto &q = c.evq[i];
+        SH_CHECK(hipEventSynchronize(q[3]));
+        for (int t = 0; t < 3; ++t) {
+            float x = 0;
+            SH_CHECK(hipEventElapsedTime(&x, q[t], q[t + 1]));
+            sum[t] += x;
+        }
+    }
+    for (int t = 0; t < 3; ++t) ms[t] = static_cast<float>(sum[t] / c.ev_count);
+    return c.ev_count;
 }
 
 extern "C" int cauchy_256_sync(void *stream) {

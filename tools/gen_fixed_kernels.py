@@ -161,6 +161,13 @@ class Body:
                     ups.append((v >> 4, v & 15, yi, b))
                     v = gmul(v, 2)
             ups.sort(key=lambda u: (u[0], u[1]))
+            if os.environ.get("SH_TABLES_FIRST"):  # experiment: build every needed entry first
+                for hi, lo, yi, b in ups:
+                    if lo:
+                        self.table_expr(0, lo, have, cur)
+                for hi, lo, yi, b in ups:
+                    if hi:
+                        self.table_expr(1, hi, have, cur)
             for hi, lo, yi, b in ups:
                 acc = f"acc[{yi}][{b}]"
                 if lo and hi:
@@ -232,9 +239,10 @@ def gen_config(k, m):
         out.append("")
     out.append(f"template <class Src>")
     out.append(f"__device__ __forceinline__ void run_{name}(int part, const Src &src, const Sink &sink) {{")
+    same = os.environ.get("SH_EXPERIMENT_SAME_CODE")  # timing experiment only: wrong results
     for p in range(len(parts)):
         kw = "if" if p == 0 else "else if"
-        out.append(f"    {kw} (part == {p}) run_{name}_p{p}(src, sink);")
+        out.append(f"    {kw} (part == {p}) run_{name}_p{0 if same else p}(src, sink);")
     out.append("}")
     out.append("}  // namespace fixed")
     out.append("}  // namespace sh")

@@ -1,13 +1,12 @@
 #!/bin/bash
-# Parity tests + bench + rocprof kernel trace of the bench (same command). Stops at the first
-# GPU crash/timeout.
+# Parity tests + bench (with CPU baseline) + rocprof kernel trace of the same bench command.
+# Stops at the first failure.
 set -u
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 step() { local name=$1 t=$2; shift 2; timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc"; tail -3 "gpurun_out/$name.log"; return $rc; }
-step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider; rc=$?
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-step bench 600 python bench.py --steps 20 --warmup 3 --cpu-seconds 5 || exit $?
+step pytest_gpu 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread || exit $?
+step bench 600 python bench.py --steps 20 --warmup 3 --cpu-seconds 10 || exit $?
 rm -rf gpurun_out/prof
 step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu || exit $?
 python3 - <<'PY'
@@ -16,4 +15,3 @@ f = glob.glob('gpurun_out/prof/**/run_kernel_stats.csv', recursive=True)[0]
 for r in csv.DictReader(open(f)):
     print(f"{r['Name'][:70]:70s} calls={r['Calls']:>4} avg_us={float(r['AverageNs'])/1e3:9.1f} pct={float(r['Percentage']):5.1f}")
 PY
-exit $rc
