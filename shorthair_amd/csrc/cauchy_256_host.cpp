@@ -176,7 +176,33 @@ hipError_t launch_fixed_batch(int k, int m, int B, int groups, const uint8_t *in
     a.geo = sh::make_geometry(B);
     a.pos = pos;
     a.rpos = rpos;
-    return sh::launch_fixed(k, m, a, dec, s);
+    if (!std::getenv("SH_DEBUG_STAMPS")) return sh::launch_fixed(k, m, a, dec, s);
+    // Diagnostic (library built with -DSH_EXPERIMENT_STAMPS): per-wave cycle stamps -> stderr.
+    const size_t nw = static_cast<size_t>(groups) * B / 8 / 4 + 4096;  // >= waves of any shape
+    unsigned long long *d = nullptr;
+    if (hipMalloc(&d, nw * 4 * 8) != hipSuccess) return hipErrorOutOfMemory;
+    hipMemsetAsync(d, 0, nw * 4 * 8, s);
+    a.dbg = d;
+    hipError_t e = sh::launch_fixed(k, m, a, dec, s);
+    std::vector<unsigned long long> h(nw * 4);
+    hipMemcpyAsync(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    hipFree(d);
+    double vm = 0, bar = 0, life = 0;
+    unsigned long long t0 = ~0ull, t1 = 0;
+    size_t n = 0;
+    for (size_t i = 0; i < nw; ++i) {
+        if (h[i * 4 + 3] == 0) continue;
+        ++n;
+        vm += h[i * 4];
+        bar += h[i * 4 + 1];
+        life += h[i * 4 + 3] - h[i * 4 + 2];
+        t0 = std::min(t0, h[i * 4 + 2]);
+        t1 = std::max(t1, h[i * 4 + 3]);
+    }
+    std::fprintf(stderr, "stamps %s: waves %zu, mean wave life %.0f, vmcnt wait %.1f%%, barrier %.1f%%, span %llu\n",
+                 dec ? "dec" : "enc", n, life / n, 100 * vm / life, 100 * bar / life, t1 - t0);
+    return e;
 }
 
 // ---- batched encode ----

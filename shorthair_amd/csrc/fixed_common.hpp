@@ -18,12 +18,16 @@
 // gfx950 (tools/dma_probe.hip): misaligned LDS-DMA sources are exact; a dword straddling the
 // buffer's num_records reads as 0.
 //
-// Pipeline (R slots). Iteration x: wait (counted vmcnt) for this wave's DMA of step x+1, join
-// the workgroup barrier (every wave's share of slot x+1 has landed, and every wave has finished
-// computing step x-1, so slot x-1 is free), issue the ds_reads of step x+1 into the second
-// register set, issue the DMA of step x+R-1 into slot x-1, then compute step x from the
-// registers read one iteration earlier: the LDS read latency hides under the compute, R-2 DMA
-// steps stay in flight. All P part-waves read the same slot: HBM sees each input byte once.
+// Pipeline (R slots, a workgroup barrier every S blocks). Iteration x issues the ds_reads of
+// block x+1 into the second register set and computes block x from the registers read one
+// iteration earlier (LDS latency under the compute). Before reading the first block of each
+// group of S, a wave waits (counted vmcnt) for its DMAs of the whole group and joins the barrier
+// -- every wave's share of those slots has landed, and every wave is past block x-1, so the
+// slots of blocks <= x-1 are free and their DMAs (blocks up to x+R-1) are issued right there.
+// R >= 2S+1 keeps R-2S-1 blocks of DMA in flight beyond the group being waited for. Fewer
+// barriers matter: measured per-wave stamps (SH_EXPERIMENT_STAMPS) showed 41 % of a wave's
+// life at the barrier with S = 1; S = 4 is 6-8 % faster. All P part-waves read the same slots:
+// HBM sees each input byte once.
 //
 // Sub-block tails. When sub = B/8 is not a multiple of 4 (175 at B = 1400) the last 4-column
 // chunk of every sub-block is shifted back by shift = 4*nq - sub bytes, on input (DMA source)
@@ -153,12 +157,29 @@ struct Src {
 
     // Wait until this wave's DMAs of steps <= T are done (I = steps issued so far), then join the
     // workgroup barrier. One asm statement: nothing is scheduled between the two.
+#ifndef SH_EXPERIMENT_STAMPS
     template <int T, int I>
     __device__ __forceinline__ static void wait() {
         constexpr int N = (I - T - 1) * S::DPW;
         static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
         asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
     }
+#else  // diagnostic build: cycles spent in the vmcnt wait and in the barrier, per wave
+    mutable unsigned long long st_vm = 0, st_bar = 0, st_t0 = 0;
+    template <int T, int I>
+    __device__ __forceinline__ void wait() const {
+        constexpr int N = (I - T - 1) * S::DPW;
+        unsigned long long t0, t1, t2;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+        asm volatile("s_barrier" ::: "memory");
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t2)::"memory");
+        if (T == 0) st_t0 = t0;
+        st_vm += t1 - t0;
+        st_bar += t2 - t1;
+    }
+#endif
 
     // Decode: the DMA source of step x depends on the group's position table (LDS). pre(x) reads
     // it one iteration before issue(x, .) needs it, so the DMA issue never waits on LDS latency.
@@ -384,6 +405,18 @@ inline hipError_t launch_shape(FixedArgs a, bool dec, hipStream_t s, void (*kern
 }  // namespace fixed
 }  // namespace sh
 
+#ifdef SH_EXPERIMENT_STAMPS
+#define SH_STAMPS_OUT(a, src)                                                                      \
+    if ((threadIdx.x & 63) == 0 && a.dbg) {                                                       \
+        unsigned long long t;                                                                     \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");               \
+        unsigned long long *d = a.dbg + (static_cast<size_t>(blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6)) * 4; \
+        d[0] = src.st_vm; d[1] = src.st_bar; d[2] = src.st_t0; d[3] = t;                          \
+    }
+#else
+#define SH_STAMPS_OUT(a, src)
+#endif
+
 // One kernel + launcher of a generated (k, m): MODE enc (DEC = false) or dec (DEC = true);
 // MINW = waves per SIMD the registers are allocated for. The host routes shapes with
 // nq % 4 != 0 (a 16-byte chunk could straddle two groups) or sub < 16 to the generic kernel.
@@ -397,6 +430,7 @@ inline hipError_t launch_shape(FixedArgs a, bool dec, hipStream_t s, void (*kern
         Sink sink;                                                                                \
         const int part = kernel_prologue<S, DEC>(a, lds, src, sink);                              \
         run_##NAME(part, src, sink);                                                              \
+        SH_STAMPS_OUT(a, src);                                                                    \
     }                                                                                             \
     hipError_t launch_##NAME##_##MODE(FixedArgs a, hipStream_t s) {                               \
         return launch_shape<Shape<K, M, P, CW, R>>(a, DEC, s, kern_##NAME##_##MODE);              \

@@ -113,6 +113,7 @@ struct FixedArgs {
     const uint8_t *pos;       // decode: [G][round4(k)] array index of original row x, 0xFF = erased
     const uint8_t *rpos;      // decode: [G][round4(m)] array index of recovery row y, 0xFF = absent
     int groups_per_wg;        // set by the launcher
+    unsigned long long *dbg;  // diagnostic builds only (SH_EXPERIMENT_STAMPS): per-wave cycle stamps
 };
 
 // Returns hipErrorNotSupported (and launches nothing) when (k, m) has no generated kernel or the

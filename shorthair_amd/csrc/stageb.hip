@@ -238,9 +238,18 @@ __global__ __launch_bounds__(256, 3) void stageb_lds(StageBArgs a) {
                 // skip; a zero coefficient simply runs snippet 0 (adds nothing)
                 const uint32_t c = ((j < 4 ? clo : chi) >> (8 * (j & 3))) & 0xffu;
                 u32x8 tmp;
+#ifndef SH_EXPERIMENT_NO_CALL
                 SH_SNIP_CALL(snip + (static_cast<uint64_t>(c) << 6), t0, t1, tmp);
+#else  // timing experiment only: the table work and accumulation without the call
+                for (int b = 0; b < 8; ++b) tmp[b] = t0[(c + b) & 15] ^ t1[(c >> 4 + b) & 15];
+#endif
+#ifndef SH_EXPERIMENT_NO_ACC
 #pragma unroll
                 for (int b = 0; b < 8; ++b) acc[j][b] ^= tmp[b];
+#else
+                if (j == 0)
+                    for (int b = 0; b < 8; ++b) acc[0][b] ^= tmp[b];
+#endif
             }
         }
 #pragma unroll

@@ -123,7 +123,7 @@ class Body:
         have.add(name)
         return name
 
-    def emit(self, R):
+    def emit(self, R, S):
         """Software-pipelined steps (see fixed_common.hpp): iteration x waits for slot x+1,
         reads it into the other register set, refills slot x-1 with block x+R-1, and computes
         step x from the registers read one iteration earlier. Sets alternate: dA (even x), dB."""
@@ -132,24 +132,28 @@ class Body:
         k = self.k
         L.append("    uint32_t dA0, dA1, dA2, dA3, dA4, dA5, dA6, dA7;")
         L.append("    uint32_t dB0, dB1, dB2, dB3, dB4, dB5, dB6, dB7;")
-        # prologue: slot 0 (steps 0..R-2 were issued by kernel_prologue)
-        L.append(f"    src.template wait<0, {min(k, R - 1)}>();")
+        # prologue: steps 0..R-2 were issued by kernel_prologue; wait for the first group
+        nxt_issue = min(k, R - 1)  # steps 0..nxt_issue-1 issued (in order)
+        L.append(f"    src.template wait<{min(k, S) - 1}, {nxt_issue}>();")
         L.append("    src.read(0, " + ", ".join(f"dA{a}" for a in range(8)) + ");")
-        if R - 1 < k:
-            L.append(f"    typename Src::Pre pre = src.pre({R - 1});")
+        if nxt_issue < k:
+            L.append(f"    typename Src::Pre pre = src.pre({nxt_issue});")
         for x in range(k):
             cur, nxt = ("dA", "dB") if x % 2 == 0 else ("dB", "dA")
             L.append(f"    // ---- input block {x}")
             # Pin the step structure: without this hipcc hoists work across steps.
             L.append("    __builtin_amdgcn_sched_barrier(0);")
             if x + 1 < k:
-                issued = min(k, R - 1 + x)
-                L.append(f"    src.template wait<{x + 1}, {issued}>();")
+                if (x + 1) % S == 0:
+                    # group boundary: the next S blocks must have landed (counted vmcnt) and every
+                    # wave must be past block x-1 (barrier), which frees the slots of blocks <= x-1
+                    L.append(f"    src.template wait<{min(k - 1, x + S)}, {nxt_issue}>();")
+                    while nxt_issue < k and nxt_issue - R <= x - 1:
+                        L.append(f"    src.issue({nxt_issue}, pre);")
+                        nxt_issue += 1
+                        if nxt_issue < k:
+                            L.append(f"    pre = src.pre({nxt_issue});")
                 L.append(f"    src.read({(x + 1) % R}, " + ", ".join(f"{nxt}{a}" for a in range(8)) + ");")
-                if x + R - 1 < k:
-                    L.append(f"    src.issue({x + R - 1}, pre);")
-                    if x + R < k:
-                        L.append(f"    pre = src.pre({x + R});")
             L.append("    {")
             have = set()
             # Updates ordered by the high-half table entry: each T1 entry is built right before
@@ -197,16 +201,20 @@ def shape(k, m):
     # (With one wave per part the code stream -- ~0.7 KB per step and part -- outweighs the data
     # stream and instruction fetch, not HBM, bounds the kernel.)
     CW = int(os.environ.get("SH_CW", str(max(1, min(8, 8 // P)))))
+    # LDS per workgroup (2 per CU): ring R slots + 2 KB store scratch per wave, <= ~76 KB
+    nw = CW * P
     slot = 8 * CW * 64 * 4
-    R = int(os.environ.get("SH_RING", str(max(3, min(8, 65536 // slot)))))
+    R = int(os.environ.get("SH_RING", str(max(3, min(14, 65536 // slot, (76 * 1024 - 2048 * nw) // slot)))))
     rows = (m + P - 1) // P
     minw = int(os.environ.get("SH_MIN_WAVES", "2" if rows > 12 else ("3" if rows > 8 else "4")))
-    return P, CW, R, minw
+    # blocks per barrier: R >= 2*SYNC + 1 keeps >= 1 group of DMA in flight past the one waited for
+    sync = int(os.environ.get("SH_SYNC", str(max(1, min(4, (R - 1) // 2 - 1)))))
+    return P, CW, R, minw, sync
 
 
 def gen_config(k, m):
     rows = generator(k, m)
-    P, CW, R, minw = shape(k, m)
+    P, CW, R, minw, sync = shape(k, m)
     per = (m + P - 1) // P
     parts = [(y0, min(m, y0 + per)) for y0 in range(0, m, per)]
     name = f"k{k}_m{m}"
@@ -220,7 +228,7 @@ def gen_config(k, m):
            "namespace fixed {",
            ""]
     for p, (y0, y1) in enumerate(parts):
-        body = Body(k, rows, y0, y1).emit(R)
+        body = Body(k, rows, y0, y1).emit(R, sync)
         nr = y1 - y0
         out.append(f"template <class Src>")
         out.append(f"__device__ __forceinline__ void run_{name}_p{p}(const Src &src, const Sink &sink) {{")

@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <algorithm>
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 typedef __attribute__((address_space(3))) void lds_void;
@@ -180,11 +181,12 @@ static float timeit(F f, int iters) {
     return ms / iters;
 }
 
-static void run(const char *name, int R, int CW, int P, int ACC, Args a, double bytes, void (*kern)(Args)) {
+static void run(const char *name, int R, int CW, int P, int ACC, Args a, double bytes, void (*kern)(Args),
+                size_t lds_pad = 0) {
     const int COLS = CW * 64;
     const long long cols = (long long)a.groups * a.nq;
     const unsigned blocks = (unsigned)((cols + COLS - 1) / COLS);
-    const size_t lds = (size_t)R * 8 * COLS * 4;
+    const size_t lds = std::max((size_t)R * 8 * COLS * 4, lds_pad);
     float ms = timeit([&] { hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * CW * P), lds, 0, a); }, 5);
     CK(hipGetLastError());
     const double valu = (double)blocks * CW * 200 * P * (16 + ACC) ;  // wave-instr
@@ -217,6 +219,8 @@ int main() {
     run("c2 p3 a88", 8, 2, 3, 88, a, bytes, k_r8_c2_p3_a88);
     run("c1 p3 a88", 8, 1, 3, 88, a, bytes, k_r8_c1_p3_a88);
     run("c1 p4 a64", 8, 1, 4, 64, a, bytes, k_r8_c1_p4_a64);
+    run("c1 p4 a64 occ4 (LDS pad)", 8, 1, 4, 64, a, bytes, k_r8_c1_p4_a64, 40 * 1024);
+    run("c1 p4 a64 occ3 (LDS pad)", 8, 1, 4, 64, a, bytes, k_r8_c1_p4_a64, 53 * 1024);
     run("c2 p4 a64", 8, 2, 4, 64, a, bytes, k_r8_c2_p4_a64);
     run("c4 p1 a128 (half rows)", 8, 4, 1, 128, a, bytes, k_r8_c4_p1_a128);
     run("c1 p4 a64 UNROLLED", 8, 1, 4, 64, a, bytes, k_unr_c1_p4_a64);
