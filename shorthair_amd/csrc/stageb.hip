@@ -22,6 +22,7 @@
 #include "snippets.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace sh {
 
@@ -272,6 +273,158 @@ __global__ __launch_bounds__(256, 3) void stageb_lds(StageBArgs a) {
     }
 }
 
+#ifdef SH_EXPERIMENT_INLINE_SNIP  // timing experiment: fixed inline snippet, no branches
+#define SH_CALLX(G) "v_bitop3_b32 v64, v64, v129, v146 bitop3:0x96\n""v_bitop3_b32 v65, v65, v132, v151 bitop3:0x96\n""v_bitop3_b32 v66, v66, v135, v156 bitop3:0x96\n""v_bitop3_b32 v67, v67, v138, v145 bitop3:0x96\n""v_bitop3_b32 v68, v68, v141, v150 bitop3:0x96\n""v_bitop3_b32 v69, v69, v128, v155 bitop3:0x96\n""v_bitop3_b32 v70, v70, v131, v144 bitop3:0x96\n""v_bitop3_b32 v71, v71, v134, v149 bitop3:0x96\n"
+#else
+#define SH_CALLX(G) "s_swappc_b64 s[40:41], %[" #G "]\n"
+#endif
+__global__ __launch_bounds__(256, 3) void stageb_acc(StageBArgs a) {
+    SH_SNIPA_TABLE(A);
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const Geometry geo = a.geo;
+    const int ncc = (geo.nq + 63) / 64;
+    const int g = blockIdx.x / ncc;
+    const int cc = blockIdx.x - g * ncc;
+    const int c0 = cc * 64;
+    const int ncols = min(64, geo.nq - c0);
+    const int nch = ncols / 4;        // 16-byte chunks per (row, sub-block)
+    const int cpb = nch * 16;         // LDS bytes per (row, sub-block)
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int e = a.e[g];
+    const int j0 = (blockIdx.y * 4 + wave) * 8;
+
+    // ---- gather the residual tile into LDS: chunk ch = (y*8 + a)*nch + t; then the group's
+    // stage-B coefficients (n_in x ldT bytes) behind it
+    const int total = a.n_in * 8 * nch;
+    const int tile = ((total + 255) / 256) * 256 * 16;
+    uint8_t *lcoef = lds + tile;
+    {
+        const long long gbase = static_cast<long long>(g) * a.in_gstride;
+        long long avail = static_cast<long long>(a.groups) * a.in_gstride + a.in_slack - gbase;
+        if (avail > 0x7FFFFFFFll) avail = 0x7FFFFFFFll;
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t *>(a.in + gbase), static_cast<short>(0), static_cast<int>(avail), 0x00020000);
+        for (int base = wave * 64; base < total; base += 256) {  // uniform
+            const int ch = base + lane;
+            uint32_t off = 0x80000000u;
+            if (ch < total) {
+                const int ya = ch / nch, t = ch - ya * nch;
+                const int y = ya >> 3, sa = ya & 7;
+                off = static_cast<uint32_t>(y) * geo.B + static_cast<uint32_t>(sa) * geo.sub +
+                      colx_off(c0 + 4 * t, geo.nq, geo.sub);
+            }
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t *)(lds + base * 16), 16, off, 0, 0, 0);
+        }
+        const int cbytes = a.n_in * a.ldT;  // multiple of 8; <= 32 * 32
+        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t *>(a.coefT + static_cast<long long>(g) * a.coefT_gstride), static_cast<short>(0),
+            cbytes, 0x00020000);
+        for (int base = wave * 64; base * 16 < cbytes; base += 256)  // uniform
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rc, (lds_void_t *)(lcoef + base * 16), 16, (base + lane) * 16, 0, 0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    if (j0 >= e) return;  // wave-uniform (after the barrier)
+
+    uint64_t snip;
+    asm volatile(
+        "s_getpc_b64 s[42:43]\n"
+        "s_add_u32 s42, s42, sh_snipa_baseA@rel32@lo+4\n"
+        "s_addc_u32 s43, s43, sh_snipa_baseA@rel32@hi+12\n"
+        "s_mov_b64 %0, s[42:43]"
+        : "=s"(snip)
+        :
+        : "s42", "s43", "scc");
+
+    const uint8_t *rd = lds + 4 * lane;
+    const uint8_t *cf = lcoef + j0;
+
+    // accumulators pinned to v[64:127] (output j at v[64+8j..]), window tables to v[128:159]
+    u32x16 a01, a23, a45, a67;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) a01[i] = a23[i] = a45[i] = a67[i] = 0;
+
+    // rows and coefficients are prefetched one input row ahead (LDS latency under the calls)
+    uint32_t d[8], dn[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) d[s] = *reinterpret_cast<const uint32_t *>(rd + s * cpb);
+    uint2 cv = *reinterpret_cast<const uint2 *>(cf);
+    for (int y = 0; y < a.n_in; ++y) {
+        const int yn = y + 1 < a.n_in ? y + 1 : y;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) dn[s] = *reinterpret_cast<const uint32_t *>(rd + (yn * 8 + s) * cpb);
+        const uint2 cvn = *reinterpret_cast<const uint2 *>(cf + yn * a.ldT);
+        const uint32_t clo = __builtin_amdgcn_readfirstlane(cv.x), chi = __builtin_amdgcn_readfirstlane(cv.y);
+        if ((clo | chi) != 0) {  // wave-uniform: no output of this wave uses input y otherwise
+            u32x16 t0, t1;
+            t0[0] = 0;
+            t1[0] = 0;
+            t0[1] = d[0]; t0[2] = d[1]; t0[4] = d[2]; t0[8] = d[3];
+            t1[1] = d[4]; t1[2] = d[5]; t1[4] = d[6]; t1[8] = d[7];
+            t0[3] = t0[1] ^ t0[2]; t0[5] = t0[1] ^ t0[4]; t0[6] = t0[2] ^ t0[4]; t0[7] = t0[3] ^ t0[4];
+            t0[9] = t0[1] ^ t0[8]; t0[10] = t0[2] ^ t0[8]; t0[11] = t0[3] ^ t0[8]; t0[12] = t0[4] ^ t0[8];
+            t0[13] = t0[5] ^ t0[8]; t0[14] = t0[6] ^ t0[8]; t0[15] = t0[7] ^ t0[8];
+            t1[3] = t1[1] ^ t1[2]; t1[5] = t1[1] ^ t1[4]; t1[6] = t1[2] ^ t1[4]; t1[7] = t1[3] ^ t1[4];
+            t1[9] = t1[1] ^ t1[8]; t1[10] = t1[2] ^ t1[8]; t1[11] = t1[3] ^ t1[8]; t1[12] = t1[4] ^ t1[8];
+            t1[13] = t1[5] ^ t1[8]; t1[14] = t1[6] ^ t1[8]; t1[15] = t1[7] ^ t1[8];
+            uint64_t tg[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                tg[j] = snip + (static_cast<uint64_t>(((j < 4 ? clo : chi) >> (8 * (j & 3))) & 0xffu) << 7);
+            // One asm block: VGPR-index mode must not see any compiler VALU between on and off.
+            asm volatile(
+                "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"
+                SH_CALLX(g0)
+                "s_set_gpr_idx_idx 8\n"
+                SH_CALLX(g1)
+                "s_set_gpr_idx_idx 16\n"
+                SH_CALLX(g2)
+                "s_set_gpr_idx_idx 24\n"
+                SH_CALLX(g3)
+                "s_set_gpr_idx_idx 32\n"
+                SH_CALLX(g4)
+                "s_set_gpr_idx_idx 40\n"
+                SH_CALLX(g5)
+                "s_set_gpr_idx_idx 48\n"
+                SH_CALLX(g6)
+                "s_set_gpr_idx_idx 56\n"
+                SH_CALLX(g7)
+                "s_set_gpr_idx_off"
+                : "+{v[64:79]}"(a01), "+{v[80:95]}"(a23), "+{v[96:111]}"(a45), "+{v[112:127]}"(a67)
+                : "{v[128:143]}"(t0), "{v[144:159]}"(t1), [g0] "s"(tg[0]), [g1] "s"(tg[1]),
+                  [g2] "s"(tg[2]), [g3] "s"(tg[3]), [g4] "s"(tg[4]), [g5] "s"(tg[5]), [g6] "s"(tg[6]),
+                  [g7] "s"(tg[7])
+                : "s40", "s41", "m0", "memory");
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) d[s] = dn[s];
+        cv = cvn;
+    }
+    uint32_t acc[8][8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        acc[0][b] = a01[b]; acc[1][b] = a01[8 + b];
+        acc[2][b] = a23[b]; acc[3][b] = a23[8 + b];
+        acc[4][b] = a45[b]; acc[5][b] = a45[8 + b];
+        acc[6][b] = a67[b]; acc[7][b] = a67[8 + b];
+    }
+
+    if (lane >= ncols) return;
+    const uint32_t col = colx_off(c0 + lane, geo.nq, geo.sub);
+    uint8_t *out = a.out + static_cast<long long>(g) * a.out_gstride + col;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (j0 + j >= e) break;
+        uint8_t *row = out + static_cast<long long>(j0 + j) * geo.B;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const uint32_t w = acc[j][b];
+            __builtin_memcpy(row + b * geo.sub, &w, 4);
+        }
+    }
+}
+
 bool stageb_lds_ok(const StageBArgs &a) {
     return a.n_in <= 32 && a.ldT <= 32 && a.geo.nq % 4 == 0 && a.geo.sub >= 16;
 }
@@ -286,7 +439,10 @@ hipError_t launch_stageb(const StageBArgs &a, int emax, hipStream_t stream) {
         const size_t cbytes = static_cast<size_t>(a.n_in) * a.ldT;  // coefficients behind the tile
         const size_t lds = ((chunks + 255) / 256) * 256 * 16 + ((cbytes + 4095) / 4096) * 4096;
         dim3 grid(static_cast<unsigned>(ncc) * a.groups, (emax + 31) / 32, 1);
-        hipLaunchKernelGGL(stageb_lds, grid, dim3(256), lds, stream, a);
+        if (std::getenv("SH_STAGEB_SNIP"))  // A/B switch: the copy-and-XOR snippet kernel
+            hipLaunchKernelGGL(stageb_lds, grid, dim3(256), lds, stream, a);
+        else
+            hipLaunchKernelGGL(stageb_acc, grid, dim3(256), lds, stream, a);
         return hipGetLastError();
     }
     dim3 grid(static_cast<unsigned>((a.geo.nq + 63) / 64) * a.groups, (emax + 31) / 32, 1);

@@ -276,6 +276,7 @@ def gen_config(k, m):
 # returns with s_setpc_b64. 256 snippets x 64 B = 16 KB, emitted inside the kernel behind an
 # s_branch (file-scope asm is dropped by HIP device compilation).
 SNIP_T0, SNIP_T1, SNIP_TMP = 100, 116, 132
+SNIPA_ACC, SNIPA_T0, SNIPA_T1 = 64, 128, 144
 
 
 def gen_snippets():
@@ -297,9 +298,28 @@ def gen_snippets():
             v = gmul(v, 2)
         lines.append('    "s_setpc_b64 s[40:41]\\n"')
     lines.append('    "sh_snip_end" #SFX ":\\n" ::: "memory")')
+    # Accumulating variant for VGPR-index mode (csrc/stageb.hip, stageb_acc): snippet c does
+    # acc[b] ^= T0[lo(c*2^b)] ^ T1[hi(c*2^b)] as 8 v_bitop3_b32 whose destination and first
+    # source are relative to M0 (s_set_gpr_idx_on ..., gpr_idx(SRC0,DST)): the caller selects the
+    # output row with s_set_gpr_idx_idx, no copy-and-XOR of a temporary. 128-byte stride.
+    acc = ['#define SH_SNIPA_ACC %d' % SNIPA_ACC, '#define SH_SNIPA_T0 %d' % SNIPA_T0,
+           '#define SH_SNIPA_T1 %d' % SNIPA_T1,
+           '#define SH_SNIPA_TABLE(SFX) asm volatile("s_branch sh_snipa_end" #SFX "\\n"',
+           '    ".p2align 7\\n"',
+           '    "sh_snipa_base" #SFX ":\\n"']
+    for c in range(256):
+        v = c
+        acc.append('    ".p2align 7\\n"')
+        for b in range(8):
+            lo, hi = v & 15, v >> 4
+            acc.append(f'    "v_bitop3_b32 v{SNIPA_ACC + b}, v{SNIPA_ACC + b}, v{SNIPA_T0 + lo}, v{SNIPA_T1 + hi} bitop3:0x96\\n"')
+            v = gmul(v, 2)
+        acc.append('    "s_setpc_b64 s[40:41]\\n"')
+    acc.append('    "sh_snipa_end" #SFX ":\\n" ::: "memory")')
     with open(os.path.join(OUTDIR, "snippets.h"), "w") as f:
         f.write(lines[0] + "\n" + lines[1] + "\n" + lines[2] + "\n" + "\n".join(lines[3:6]) + "\n"
                 + " \\\n".join(lines[6:]) + "\n")
+        f.write("\n".join(acc[:3]) + "\n" + " \\\n".join(acc[3:]) + "\n")
 
 
 def main(argv=()):
