@@ -44,6 +44,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline sample wall time")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--root-steps", type=int, default=3,
+                   help="N>1: steps of the root-resident variant (RCCL scatter -> encode -> gather); 0 = skip")
     return p.parse_args()
 
 
@@ -97,6 +99,35 @@ def cpu_baseline(k, m, B, e_fixed, seconds, threads):
                 sample=f"{sum(counts)} encode+decode group pairs (k={k} m={m} B={B} e={e_fixed or 'rand'}) "
                        f"over {dt:.1f}s on {threads} host threads, ctypes-released GIL, "
                        f"reference built -O3 -march=x86-64-v3, gf256_init not called (as shipped)")
+
+
+def root_resident(args, sh, shd, dist, torch, rank, world, G, k, m, B, s, enc_in, enc_out):
+    """Groups start and end on rank 0's GPU: one RCCL scatter of the data shards over xGMI,
+    encode on every GPU, one RCCL gather of the recovery shards (north_star's root-resident
+    flow). Reported beside the main line, never as `value`."""
+    root_in = root_rec = None
+    if rank == 0:
+        root_in = torch.empty((world * G, k, B), dtype=torch.uint8, device="cuda")
+        root_rec = torch.empty((world * G, m, B), dtype=torch.uint8, device="cuda")
+        sh.fill_synthetic(root_in, k, B, world * G, 0, 0xBE, s)
+    torch.cuda.synchronize()
+    shd.scatter_groups(enc_in, root_in)  # warm-up
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.root_steps):
+        shd.scatter_groups(enc_in, root_in)
+        assert sh.encode_batch(k, m, B, G, enc_in, enc_out, s) == 0
+        shd.gather_groups(enc_out, root_rec)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t_root = shd.max_over_ranks(time.perf_counter() - t0, device="cuda")
+    if rank != 0:
+        return None
+    return {"op": "RCCL scatter + encode + RCCL gather, groups resident on rank 0",
+            "steps": args.root_steps, "ms_per_step": round(t_root / args.root_steps * 1e3, 4),
+            "GiBps": round(world * G * (k + m) * B * args.root_steps / t_root / 2**30, 3),
+            "root_shard_roundtrip_ok": bool(torch.equal(root_rec[:G], enc_out))}
 
 
 def main():
@@ -184,15 +215,19 @@ def main():
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     stages = sh.profile_read() or (float("nan"),) * 3
     sh.profile(0)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        tot = torch.tensor([dec_bytes], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        dec_bytes_all = float(tot.item())
-    else:
-        dec_bytes_all = float(dec_bytes)
+    from shorthair_amd import dist as shd
+    elapsed = shd.max_over_ranks(elapsed, device="cuda")
+    dec_bytes_all = shd.sum_over_ranks(dec_bytes, device="cuda")
+
+    # ---- root-resident variant (N > 1): groups start and end on rank 0's GPU; one RCCL scatter of
+    # the data shards over xGMI, encode on every GPU, one RCCL gather of the recovery shards.
+    # Reported beside the main line, never as `value`.
+    root_res = None
+    if world > 1 and args.root_steps > 0:
+        try:
+            root_res = root_resident(args, sh, shd, dist, torch, rank, world, G, k, m, B, s, enc_in, enc_out)
+        except Exception as exc:  # never lose the main line over the side measurement
+            root_res = {"error": f"{type(exc).__name__}: {exc}"}
     enc_bytes_all = float(enc_bytes) * world
     total = (enc_bytes_all + dec_bytes_all) * args.steps
     value = total / elapsed / 2**30
@@ -235,6 +270,8 @@ def main():
                          "alg_bytes_per_launch": kb, "launch_ms": round(dom[1], 4)},
             "cpu_baseline": cpu,
         }
+        if root_res is not None:
+            line["root_resident"] = root_res
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
