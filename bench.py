@@ -56,8 +56,7 @@ def cpu_baseline(k, m, B, e_fixed, seconds, threads):
     groups (same synthetic generator as the GPU run) until `seconds` elapse.
     """
     try:
-        from oracle import pyoracle as po
-        ref = po.reference()
+            ref = po.reference()
     except Exception:
         ref = None
     kind = "reference"
@@ -158,11 +157,10 @@ def main():
     sh.fill_synthetic(enc_in, k, B, G, g0, 0xBE, s)
     sh.encode_batch(k, m, B, G, enc_in, enc_out, s)
     # decode input: each group with its erasure pattern (survivors then recovery rows)
-    from oracle import pyoracle as po  # only for the erasure-pattern generator (host ints)
     rows_np = np.zeros((G, k), np.uint8)
     es = np.zeros(G, np.int64)
     for g in range(G):
-        es[g], rows_np[g] = po.erasure_pattern(g0 + g, k, m, 0xBE, args.erasures)
+        es[g], rows_np[g] = sh.erasure_pattern(g0 + g, k, m, 0xBE, args.erasures)
     rows = torch.from_numpy(rows_np).cuda()
     whole = torch.cat([enc_in, enc_out], dim=1)
     dec_in = whole[torch.arange(G, device="cuda")[:, None], rows.long()].contiguous()

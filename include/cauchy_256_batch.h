@@ -54,6 +54,13 @@ int cauchy_256_batch_reserve(int k, int m, int block_bytes, int groups);
 int cauchy_256_fill_synthetic(void *d_out, int n, int block_bytes, int groups,
                               unsigned long long g0, unsigned long long cfg, void *stream);
 
+/* Synthetic erasure pattern of group g (host only, no GPU): rows_out[0..k-1] = the decoder's
+ * input rows (survivors ascending, then e chosen recovery rows k+y ascending), same stream as the
+ * test oracle; e = e_fixed (clamped to min(k, m)) or PCG-random in [1, min(k, m)] when 0.
+ * Returns e, or -1 on bad arguments. */
+int cauchy_256_erasure_pattern(unsigned long long g, int k, int m, unsigned long long cfg, int e_fixed,
+                               unsigned char *rows_out);
+
 /* The library's private stream (used by the single-group calls) and a synchronize helper for
  * callers without HIP. */
 void *cauchy_256_default_stream(void);

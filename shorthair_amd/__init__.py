@@ -14,7 +14,7 @@ import os
 
 __all__ = ["lib", "Block", "CAUCHY_256_VERSION", "cauchy_256_init", "cauchy_256_encode",
            "cauchy_256_decode", "encode_batch", "decode_batch", "decode_batch_out",
-           "fill_synthetic", "batch_reserve", "default_stream", "sync", "LIB_PATH",
+           "fill_synthetic", "erasure_pattern", "batch_reserve", "default_stream", "sync", "LIB_PATH",
            "EXPORTED_SYMBOLS"]
 
 CAUCHY_256_VERSION = 2
@@ -26,6 +26,7 @@ EXPORTED_SYMBOLS = [
     "_cauchy_256_init", "cauchy_256_encode", "cauchy_256_decode",
     "cauchy_256_batch_init", "cauchy_256_encode_batch", "cauchy_256_decode_batch",
     "cauchy_256_decode_batch_out", "cauchy_256_batch_reserve", "cauchy_256_fill_synthetic",
+    "cauchy_256_erasure_pattern",
     "cauchy_256_default_stream", "cauchy_256_sync", "cauchy_256_profile", "cauchy_256_profile_read",
 ]
 
@@ -61,6 +62,9 @@ lib.cauchy_256_batch_reserve.restype = _c.c_int
 lib.cauchy_256_fill_synthetic.argtypes = [_c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
                                           _c.c_ulonglong, _c.c_ulonglong, _c.c_void_p]
 lib.cauchy_256_fill_synthetic.restype = _c.c_int
+lib.cauchy_256_erasure_pattern.argtypes = [_c.c_ulonglong, _c.c_int, _c.c_int, _c.c_ulonglong, _c.c_int,
+                                           _c.c_void_p]
+lib.cauchy_256_erasure_pattern.restype = _c.c_int
 lib.cauchy_256_default_stream.argtypes = []
 lib.cauchy_256_default_stream.restype = _c.c_void_p
 lib.cauchy_256_sync.argtypes = [_c.c_void_p]
@@ -134,6 +138,16 @@ def decode_batch_out(k, m, block_bytes, groups, blocks, rows, out, out_rows, out
 def fill_synthetic(out, n, block_bytes, groups, g0, cfg, stream=None):
     return _check(lib.cauchy_256_fill_synthetic(_ptr(out), n, block_bytes, groups, g0, cfg,
                                                 _stream(stream)), "fill_synthetic")
+
+
+def erasure_pattern(g, k, m, cfg, e_fixed=0):
+    """Synthetic decoder input rows of group g (host, no GPU): returns (e, rows uint8[k])."""
+    import numpy as np
+    rows = np.zeros(k, np.uint8)
+    e = lib.cauchy_256_erasure_pattern(g, k, m, cfg, e_fixed, rows.ctypes.data)
+    if e < 0:
+        raise ValueError("erasure_pattern: bad arguments")
+    return e, rows
 
 
 def batch_reserve(k, m, block_bytes, groups):

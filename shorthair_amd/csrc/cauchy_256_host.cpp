@@ -301,7 +301,34 @@ hipError_t launch_stage_b(Context &, const DecodeWS &w, int n_in, int B, int gro
     b.ldT = w.ldB;
     b.groups = groups;
     b.geo = sh::make_geometry(B);
-    return sh::launch_stageb(b, w.emax, s);
+    if (!std::getenv("SH_DEBUG_STAMPS")) return sh::launch_stageb(b, w.emax, s);
+    // Diagnostic (library built with -DSH_EXPERIMENT_STAMPS): per-wave phase stamps -> stderr.
+    const size_t nw = static_cast<size_t>(groups) * ((B / 8 / 4 + 63) / 64) * ((w.emax + 31) / 32) * 4;
+    unsigned long long *d = nullptr;
+    if (hipMalloc(&d, nw * 8 * 8) != hipSuccess) return hipErrorOutOfMemory;
+    hipMemsetAsync(d, 0, nw * 8 * 8, s);
+    b.dbg = d;
+    hipError_t e = sh::launch_stageb(b, w.emax, s);
+    std::vector<unsigned long long> h(nw * 8);
+    hipMemcpyAsync(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    hipFree(d);
+    double ph[5] = {0, 0, 0, 0, 0};
+    unsigned long long t0 = ~0ull, t1 = 0;
+    size_t n = 0;
+    for (size_t i = 0; i < nw; ++i) {
+        const unsigned long long *r = &h[i * 8];
+        if (r[5] == 0) continue;
+        ++n;
+        for (int j = 0; j < 5; ++j) ph[j] += static_cast<double>(r[j + 1] - r[j]);
+        t0 = std::min(t0, r[0]);
+        t1 = std::max(t1, r[5]);
+    }
+    std::fprintf(stderr,
+                 "stamps stageB: waves %zu, mean cycles: prologue %.0f, dma %.0f, rows %.0f, stores %.0f, "
+                 "drain %.0f; span %llu\n",
+                 n, ph[0] / n, ph[1] / n, ph[2] / n, ph[3] / n, ph[4] / n, t1 - t0);
+    return e;
 }
 
 // Common decode core (m >= 2, valid params): writes recovered blocks densely into `dst`
@@ -494,6 +521,45 @@ extern "C" int cauchy_256_fill_synthetic(void *d_out, int n, int block_bytes, in
     SH_CHECK(sh::launch_fill(static_cast<uint8_t *>(d_out), static_cast<long long>(n) * block_bytes,
                              n, block_bytes, groups, g0, cfg, pick(stream)));
     return 0;
+}
+
+// Synthetic erasure pattern of group g (host integers, no GPU): the same PCG32 stream and
+// partial Fisher-Yates picks as the test oracle's generator (oracle/cauchy_oracle.c), so the
+// benchmark's decode inputs match the parity tests'. Survivors ascending, then the chosen
+// recovery rows (k + y) ascending; returns the erasure count e.
+extern "C" int cauchy_256_erasure_pattern(unsigned long long g, int k, int m, unsigned long long cfg,
+                                          int e_fixed, unsigned char *rows_out) {
+    if (k <= 0 || m <= 0 || k + m > 256 || !rows_out) return -1;
+    const uint64_t inc = (static_cast<uint64_t>(g) << 1) | 1ull;
+    uint64_t state = 0;
+    auto next = [&]() {
+        const uint64_t old = state;
+        state = old * 6364136223846793005ull + inc;
+        const uint32_t xs = static_cast<uint32_t>(((old >> 18) ^ old) >> 27);
+        const uint32_t rot = static_cast<uint32_t>(old >> 59);
+        return (xs >> rot) | (xs << ((32u - rot) & 31u));
+    };
+    next();
+    state += cfg ^ 0xE7A5ull;
+    next();
+    const int emax = std::min(k, m);
+    const int e = e_fixed > 0 ? std::min(e_fixed, emax) : 1 + static_cast<int>(next() % static_cast<uint32_t>(emax));
+    uint8_t pk[256], pm[256];
+    bool lost[256] = {}, used[256] = {};
+    for (int i = 0; i < k; ++i) pk[i] = static_cast<uint8_t>(i);
+    for (int i = 0; i < m; ++i) pm[i] = static_cast<uint8_t>(i);
+    for (int i = 0; i < e; ++i) {
+        std::swap(pk[i], pk[i + static_cast<int>(next() % static_cast<uint32_t>(k - i))]);
+        std::swap(pm[i], pm[i + static_cast<int>(next() % static_cast<uint32_t>(m - i))]);
+        lost[pk[i]] = true;
+        used[pm[i]] = true;
+    }
+    int n = 0;
+    for (int x = 0; x < k; ++x)
+        if (!lost[x]) rows_out[n++] = static_cast<uint8_t>(x);
+    for (int y = 0; y < m; ++y)
+        if (used[y]) rows_out[n++] = static_cast<uint8_t>(k + y);
+    return e;
 }
 
 extern "C" void *cauchy_256_default_stream(void) {

@@ -97,6 +97,7 @@ struct StageBArgs {
     int ldT;
     int groups;
     Geometry geo;
+    unsigned long long *dbg;  // diagnostic builds only (SH_EXPERIMENT_STAMPS): per-wave phase stamps
 };
 hipError_t launch_stageb(const StageBArgs &a, int emax, hipStream_t stream);
 

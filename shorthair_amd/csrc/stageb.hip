@@ -278,6 +278,31 @@ __global__ __launch_bounds__(256, 3) void stageb_lds(StageBArgs a) {
 #else
 #define SH_CALLX(G) "s_swappc_b64 s[40:41], %[" #G "]\n"
 #endif
+#ifdef SH_EXPERIMENT_NO_ROWS  // timing experiment: wrong results, no per-row compute
+#define SH_ROWS_ON false
+#else
+#define SH_ROWS_ON true
+#endif
+#ifdef SH_EXPERIMENT_NO_GPRIDX  // timing experiment: wrong results, no VGPR-index mode
+#define SH_GI_ON ""
+#define SH_GI_IDX(n) ""
+#define SH_GI_OFF ""
+#else
+#define SH_GI_ON "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"
+#define SH_GI_IDX(n) "s_set_gpr_idx_idx " n "\n"
+#define SH_GI_OFF "s_set_gpr_idx_off"
+#endif
+#ifdef SH_EXPERIMENT_STAMPS
+#define SH_BSTAMP(i)                                                                               \
+    do {                                                                                           \
+        unsigned long long t_;                                                                     \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
+        st_[i] = t_;                                                                               \
+    } while (0)
+#else
+#define SH_BSTAMP(i)
+#endif
+
 __global__ __launch_bounds__(256, 3) void stageb_acc(StageBArgs a) {
     SH_SNIPA_TABLE(A);
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -291,7 +316,15 @@ __global__ __launch_bounds__(256, 3) void stageb_acc(StageBArgs a) {
     const int cpb = nch * 16;         // LDS bytes per (row, sub-block)
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
+#ifdef SH_EXPERIMENT_STAMPS
+    unsigned long long st_[6];
+#endif
+    SH_BSTAMP(0);
     const int e = a.e[g];
+#ifdef SH_EXPERIMENT_STAMPS
+    asm volatile("" ::"s"(e));
+#endif
+    SH_BSTAMP(1);
     const int j0 = (blockIdx.y * 4 + wave) * 8;
 
     // ---- gather the residual tile into LDS: chunk ch = (y*8 + a)*nch + t; then the group's
@@ -326,6 +359,7 @@ __global__ __launch_bounds__(256, 3) void stageb_acc(StageBArgs a) {
         __syncthreads();
     }
     if (j0 >= e) return;  // wave-uniform (after the barrier)
+    SH_BSTAMP(2);
 
     uint64_t snip;
     asm volatile(
@@ -356,7 +390,7 @@ __global__ __launch_bounds__(256, 3) void stageb_acc(StageBArgs a) {
         for (int s = 0; s < 8; ++s) dn[s] = *reinterpret_cast<const uint32_t *>(rd + (yn * 8 + s) * cpb);
         const uint2 cvn = *reinterpret_cast<const uint2 *>(cf + yn * a.ldT);
         const uint32_t clo = __builtin_amdgcn_readfirstlane(cv.x), chi = __builtin_amdgcn_readfirstlane(cv.y);
-        if ((clo | chi) != 0) {  // wave-uniform: no output of this wave uses input y otherwise
+        if (SH_ROWS_ON && (clo | chi) != 0) {  // wave-uniform: no output of this wave uses input y otherwise
             u32x16 t0, t1;
             t0[0] = 0;
             t1[0] = 0;
@@ -374,23 +408,23 @@ __global__ __launch_bounds__(256, 3) void stageb_acc(StageBArgs a) {
                 tg[j] = snip + (static_cast<uint64_t>(((j < 4 ? clo : chi) >> (8 * (j & 3))) & 0xffu) << 7);
             // One asm block: VGPR-index mode must not see any compiler VALU between on and off.
             asm volatile(
-                "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"
+                SH_GI_ON
                 SH_CALLX(g0)
-                "s_set_gpr_idx_idx 8\n"
+                SH_GI_IDX("8")
                 SH_CALLX(g1)
-                "s_set_gpr_idx_idx 16\n"
+                SH_GI_IDX("16")
                 SH_CALLX(g2)
-                "s_set_gpr_idx_idx 24\n"
+                SH_GI_IDX("24")
                 SH_CALLX(g3)
-                "s_set_gpr_idx_idx 32\n"
+                SH_GI_IDX("32")
                 SH_CALLX(g4)
-                "s_set_gpr_idx_idx 40\n"
+                SH_GI_IDX("40")
                 SH_CALLX(g5)
-                "s_set_gpr_idx_idx 48\n"
+                SH_GI_IDX("48")
                 SH_CALLX(g6)
-                "s_set_gpr_idx_idx 56\n"
+                SH_GI_IDX("56")
                 SH_CALLX(g7)
-                "s_set_gpr_idx_off"
+                SH_GI_OFF
                 : "+{v[64:79]}"(a01), "+{v[80:95]}"(a23), "+{v[96:111]}"(a45), "+{v[112:127]}"(a67)
                 : "{v[128:143]}"(t0), "{v[144:159]}"(t1), [g0] "s"(tg[0]), [g1] "s"(tg[1]),
                   [g2] "s"(tg[2]), [g3] "s"(tg[3]), [g4] "s"(tg[4]), [g5] "s"(tg[5]), [g6] "s"(tg[6]),
@@ -401,6 +435,7 @@ __global__ __launch_bounds__(256, 3) void stageb_acc(StageBArgs a) {
         for (int s = 0; s < 8; ++s) d[s] = dn[s];
         cv = cvn;
     }
+    SH_BSTAMP(3);
     uint32_t acc[8][8];
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
@@ -410,7 +445,7 @@ __global__ __launch_bounds__(256, 3) void stageb_acc(StageBArgs a) {
         acc[6][b] = a67[b]; acc[7][b] = a67[8 + b];
     }
 
-    if (lane >= ncols) return;
+    if (lane < ncols) {
     const uint32_t col = colx_off(c0 + lane, geo.nq, geo.sub);
     uint8_t *out = a.out + static_cast<long long>(g) * a.out_gstride + col;
 #pragma unroll
@@ -422,7 +457,16 @@ __global__ __launch_bounds__(256, 3) void stageb_acc(StageBArgs a) {
             const uint32_t w = acc[j][b];
             __builtin_memcpy(row + b * geo.sub, &w, 4);
         }
+    }    }
+#ifdef SH_EXPERIMENT_STAMPS
+    SH_BSTAMP(4);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    SH_BSTAMP(5);
+    if (lane == 0 && a.dbg) {
+        unsigned long long *d = a.dbg + ((static_cast<size_t>(blockIdx.y) * gridDim.x + blockIdx.x) * 4 + wave) * 8;
+        for (int t = 0; t < 6; ++t) d[t] = st_[t];
     }
+#endif
 }
 
 bool stageb_lds_ok(const StageBArgs &a) {

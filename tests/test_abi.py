@@ -95,3 +95,17 @@ def test_c_caller_runs_on_gpu(tmp_path):
     assert res.returncode == 0, res.stdout + res.stderr
     # row 1 was recovery row k+1 = 3 -> receives the missing original row 1
     assert "rc=0 row=1" in res.stdout
+
+
+@pytest.mark.parametrize("k,m,e_fixed", [(200, 32, 32), (200, 32, 0), (28, 4, 0), (3, 250, 0), (1, 1, 0),
+                                         (64, 16, 7)])
+def test_synthetic_erasure_pattern_matches_oracle(k, m, e_fixed):
+    """The library's host-side pattern generator (bench.py's decode inputs) reproduces the test
+    oracle's stream exactly, so the benchmark decodes what the parity tests check."""
+    import shorthair_amd
+    from oracle import pyoracle as po
+    for g in (0, 1, 17, 8191, 123456789):
+        e1, r1 = shorthair_amd.erasure_pattern(g, k, m, 0xBE, e_fixed)
+        e2, r2 = po.erasure_pattern(g, k, m, 0xBE, e_fixed)
+        assert e1 == e2 and (r1 == r2).all()
+    assert shorthair_amd.lib.cauchy_256_erasure_pattern(0, 200, 57, 0, 0, None) == -1

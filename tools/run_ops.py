@@ -24,7 +24,6 @@ def main():
     a = p.parse_args()
     import torch
     import shorthair_amd as sh
-    from oracle import pyoracle as po
     k, m, B, G = a.k, a.m, a.block, a.groups
     sh.cauchy_256_init()
     data = torch.empty((G, k, B), dtype=torch.uint8, device="cuda")
@@ -34,7 +33,7 @@ def main():
     if a.op in ("decode", "both"):
         rows = np.zeros((G, k), np.uint8)
         for g in range(G):
-            _, rows[g] = po.erasure_pattern(g, k, m, 0xBE, a.erasures)
+            _, rows[g] = sh.erasure_pattern(g, k, m, 0xBE, a.erasures)
         d_rows = torch.from_numpy(rows).cuda()
         whole = torch.cat([data, rec], dim=1)
         blocks = whole[torch.arange(G, device="cuda")[:, None], d_rows.long()].contiguous()
