@@ -175,11 +175,17 @@ struct Src {
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
         asm volatile("s_barrier" ::: "memory");
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t2)::"memory");
-        if (T == 0) st_t0 = t0;
+        if (st_t0 == 0) st_t0 = t0;
         st_vm += t1 - t0;
         st_bar += t2 - t1;
     }
 #endif
+
+    // After the last step: every wave's reads of the ring are done before any wave writes its
+    // store scratch (which aliases the ring).
+    __device__ __forceinline__ static void release() {
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
 
     // Decode: the DMA source of step x depends on the group's position table (LDS). pre(x) reads
     // it one iteration before issue(x, .) needs it, so the DMA issue never waits on LDS latency.
@@ -366,7 +372,10 @@ __device__ __forceinline__ int kernel_prologue(const FixedArgs &a, uint8_t *lds,
     w.q = static_cast<int>(col - static_cast<long long>(g) * nq);
     w.gl = g - w.g_first;
     w.valid = g < a.groups;
-    uint8_t *lds_pos = lds + S::R * S::SLOT + S::NW * 2048;
+    // The store scratch (2 KB per wave) aliases the start of the ring: it is used only after the
+    // last step, behind Src::release()'s barrier, so the ring gets that LDS as extra slots.
+    static_assert(S::R * S::SLOT >= S::NW * 2048, "scratch must fit inside the ring");
+    uint8_t *lds_pos = lds + S::R * S::SLOT;
     if (DEC) {
         const int ng = a.groups_per_wg;
         constexpr int TW = (S::KP + S::MP) / 4;
@@ -384,8 +393,8 @@ __device__ __forceinline__ int kernel_prologue(const FixedArgs &a, uint8_t *lds,
         __syncthreads();
     }
     src.init(a, w, lds, lds_pos);
-    if (DEC) src.init_items(a, w, lds + S::R * S::SLOT + w.wave * 2048);
-    sink.init(a, w, lds + S::R * S::SLOT + w.wave * 2048);
+    if (DEC) src.init_items(a, w, lds + w.wave * 2048);
+    sink.init(a, w, lds + w.wave * 2048);
 #pragma unroll
     for (int x = 0; x < S::R - 1 && x < S::K; ++x) src.issue(x, src.pre(x));
     return part;
@@ -396,7 +405,7 @@ inline hipError_t launch_shape(FixedArgs a, bool dec, hipStream_t s, void (*kern
     a.groups_per_wg = (S::COLS - 1) / a.geo.nq + 2;
     const long long cols = static_cast<long long>(a.groups) * a.geo.nq;
     const unsigned blocks = static_cast<unsigned>((cols + S::COLS - 1) / S::COLS);
-    const size_t lds = static_cast<size_t>(S::R) * S::SLOT + S::NW * 2048 +  // ring + store scratch
+    const size_t lds = static_cast<size_t>(S::R) * S::SLOT +  // ring (store scratch aliases it)
                        (dec ? static_cast<size_t>(a.groups_per_wg) * (S::KP + S::MP) : 0);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(S::NT), lds, s, a);
     return hipGetLastError();
