@@ -201,10 +201,12 @@ def shape(k, m):
     # (With one wave per part the code stream -- ~0.7 KB per step and part -- outweighs the data
     # stream and instruction fetch, not HBM, bounds the kernel.)
     CW = int(os.environ.get("SH_CW", str(max(1, min(8, 8 // P)))))
-    # LDS per workgroup (2 per CU): ring R slots + 2 KB store scratch per wave, <= ~76 KB
+    # LDS per workgroup (2 per CU): ring of R slots, <= ~76 KB (the 2 KB per wave of store
+    # scratch aliases the ring after the last step)
     nw = CW * P
     slot = 8 * CW * 64 * 4
-    R = int(os.environ.get("SH_RING", str(max(3, min(14, 65536 // slot, (76 * 1024 - 2048 * nw) // slot)))))
+    rmax = int(os.environ.get("SH_RING_MAX", "19"))
+    R = int(os.environ.get("SH_RING", str(max(3, min(rmax, 65536 // slot, (76 * 1024) // slot)))))
     rows = (m + P - 1) // P
     minw = int(os.environ.get("SH_MIN_WAVES", "2" if rows > 12 else ("3" if rows > 8 else "4")))
     # blocks per barrier: R >= 2*SYNC + 1 keeps >= 1 group of DMA in flight past the one waited for
@@ -215,8 +217,13 @@ def shape(k, m):
 def gen_config(k, m):
     rows = generator(k, m)
     P, CW, R, minw, sync = shape(k, m)
-    per = (m + P - 1) // P
-    parts = [(y0, min(m, y0 + per)) for y0 in range(0, m, per)]
+    # balanced parts: sizes differ by at most one row (the slowest part paces the barriers)
+    base, extra = divmod(m, P)
+    parts, y0 = [], 0
+    for p in range(P):
+        n = base + (1 if p < extra else 0)
+        parts.append((y0, y0 + n))
+        y0 += n
     name = f"k{k}_m{m}"
     out = [f"// GENERATED by tools/gen_fixed_kernels.py -- do not edit. (k={k}, m={m})",
            "// Compile-time-scheduled windowed bitmatrix product for one generator; see the",
@@ -239,6 +246,7 @@ def gen_config(k, m):
         out.append(body)
         out.append("    __builtin_amdgcn_sched_barrier(0);")
         out.append(f"    // epilogue: (decode) + received recovery rows, end fix-up, store rows {y0}..{y1 - 1}")
+        out.append("    src.release();  // the store scratch aliases the ring")
         out.append(f"    src.template epilogue<{y0}, {nr}>(acc);")
         for yi in range(nr):
             out.append("    __builtin_amdgcn_sched_barrier(0);")
