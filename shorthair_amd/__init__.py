@@ -21,13 +21,15 @@ CAUCHY_256_VERSION = 2
 LIB_PATH = os.environ.get("SH_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                          "libcauchy256.so")
 
-# Every symbol declared in include/cauchy_256.h and include/cauchy_256_batch.h.
+# Every function declared in include/*.h (cauchy_256.h, cauchy_256_batch.h, gf256.h).
 EXPORTED_SYMBOLS = [
     "_cauchy_256_init", "cauchy_256_encode", "cauchy_256_decode",
     "cauchy_256_batch_init", "cauchy_256_encode_batch", "cauchy_256_decode_batch",
     "cauchy_256_decode_batch_out", "cauchy_256_batch_reserve", "cauchy_256_fill_synthetic",
     "cauchy_256_erasure_pattern",
     "cauchy_256_default_stream", "cauchy_256_sync", "cauchy_256_profile", "cauchy_256_profile_read",
+    "gf256_init_", "gf256_add_mem", "gf256_add2_mem", "gf256_addset_mem", "gf256_mul_mem",
+    "gf256_muladd_mem", "gf256_memswap",
 ]
 
 if not os.path.exists(LIB_PATH):

@@ -13,6 +13,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, os.environ.get("SH_LIB_NAME", "libcauchy256.so"))
 SOURCES = ["kernels.hip", "stageb.hip", "fixed_dispatch.cpp", "cauchy_256_host.cpp"]
+HOST_SOURCES = ["gf256_host.cpp"]  # plain host C++ (no HIP): compiled with the host compiler
+CXX = os.environ.get("CXX", "g++")
 GEN_DIR = os.path.join(CSRC, os.environ.get("SH_GEN_DIR", "gen"))
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SH_OFFLOAD_ARCH", "gfx950")
@@ -56,9 +58,14 @@ def _compile(src, verbose):
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(
             os.path.getmtime(src), os.path.getmtime(os.path.join(CSRC, "fixed_common.hpp")),
             *( [os.path.getmtime(src[:-8] + ".inc")] if src.endswith(("_enc.hip", "_dec.hip")) else []),
-            os.path.getmtime(os.path.join(CSRC, "kernels.hpp"))):
+            os.path.getmtime(os.path.join(CSRC, "kernels.hpp")),
+            *[os.path.getmtime(os.path.join(HERE, "..", "include", h))
+              for h in os.listdir(os.path.join(HERE, "..", "include"))]):
         return obj, None
-    cmd = [HIPCC] + FLAGS + [f"-I{GEN_DIR}", "-c", src, "-o", obj]
+    if os.path.basename(src) in HOST_SOURCES:
+        cmd = [CXX, "-O3", "-std=c++17", "-fPIC", "-Wall", "-c", src, "-o", obj]
+    else:
+        cmd = [HIPCC] + FLAGS + [f"-I{GEN_DIR}", "-c", src, "-o", obj]
     if verbose:
         print(" ".join(cmd), flush=True)
     return obj, subprocess.Popen(cmd)
@@ -80,7 +87,7 @@ def build(force=False, verbose=True, jobs=None):
         for f in os.listdir(OBJ_DIR):
             os.remove(os.path.join(OBJ_DIR, f))
     jobs = jobs or max(1, min(8, os.cpu_count() or 1))
-    srcs = _gen_sources() + [os.path.join(CSRC, s) for s in SOURCES]
+    srcs = _gen_sources() + [os.path.join(CSRC, s) for s in SOURCES + HOST_SOURCES]
     objs, running = [], []
     for src in srcs:
         while len(running) >= jobs:
