@@ -44,6 +44,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline sample wall time")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--host-calls", type=int, default=50, help="single-group ABI calls timed (0 = skip)")
+    p.add_argument("--host-groups", type=int, default=1024, help="groups of the pinned-host batch leg")
     p.add_argument("--root-steps", type=int, default=3,
                    help="N>1: steps of the root-resident variant (RCCL scatter -> encode -> gather); 0 = skip")
     return p.parse_args()
@@ -128,6 +130,62 @@ def root_resident(args, sh, shd, dist, torch, rank, world, G, k, m, B, s, enc_in
             "steps": args.root_steps, "ms_per_step": round(t_root / args.root_steps * 1e3, 4),
             "GiBps": round(world * G * (k + m) * B * args.root_steps / t_root / 2**30, 3),
             "root_shard_roundtrip_ok": bool(torch.equal(root_rec[:G], enc_out))}
+
+
+def host_path(args, sh, torch, k, m, B, s):
+    """PCIe-inclusive rates (never `value`): (1) the reference-shaped single-group ABI on host
+    pointers (cauchy_256_encode / cauchy_256_decode: pinned staging, H2D, kernels, D2H per call);
+    (2) a batch that starts and ends in pinned host memory: H2D of the data, encode, D2H of the
+    recovery blocks, timed on the stream as one pipeline."""
+    import ctypes
+    out = {}
+    rng = np.random.default_rng(7)
+    data = rng.integers(0, 256, size=(k, B), dtype=np.uint8)
+    rec = np.empty((m, B), np.uint8)
+    ptrs = [data[x].ctypes.data for x in range(k)]
+    n1 = args.host_calls
+    assert sh.cauchy_256_encode(k, m, ptrs, rec.ctypes.data, B) == 0  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(n1):
+        sh.cauchy_256_encode(k, m, ptrs, rec.ctypes.data, B)
+    t_enc = (time.perf_counter() - t0) / n1
+    # decode: e = m lost originals, fresh block copies per call prepared outside the timed loop
+    e = min(m, k)
+    whole = np.concatenate([data, rec])
+    rows = list(range(e, k)) + list(range(k, k + e))
+    sets = []
+    for _ in range(n1):
+        bufs = [whole[r].copy() for r in rows]
+        arr = (sh.Block * k)(*[sh.Block(b.ctypes.data, r) for b, r in zip(bufs, rows)])
+        sets.append((bufs, arr))
+    t0 = time.perf_counter()
+    for bufs, arr in sets:
+        sh.cauchy_256_decode(k, m, arr, B)
+    t_dec = (time.perf_counter() - t0) / n1
+    ok = all(np.array_equal(sets[-1][0][k - e + i], data[i]) for i in range(e))
+    out["single_group"] = {"encode_us": round(t_enc * 1e6, 1), "decode_us": round(t_dec * 1e6, 1),
+                           "GiBps": round(2 * (k + m) * B / (t_enc + t_dec) / 2**30, 4),
+                           "calls": n1, "decode_ok": bool(ok)}
+    G = args.host_groups
+    h_in = torch.empty((G, k, B), dtype=torch.uint8, pin_memory=True)
+    h_rec = torch.empty((G, m, B), dtype=torch.uint8, pin_memory=True)
+    d_in = torch.empty((G, k, B), dtype=torch.uint8, device="cuda")
+    d_rec = torch.empty((G, m, B), dtype=torch.uint8, device="cuda")
+    sh.fill_synthetic(d_in, k, B, G, 0, 0xBE, s)
+    h_in.copy_(d_in)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    for it in range(3):  # first pass warms up
+        ev[0].record()
+        d_in.copy_(h_in, non_blocking=True)
+        sh.encode_batch(k, m, B, G, d_in, d_rec, s)
+        h_rec.copy_(d_rec, non_blocking=True)
+        ev[1].record()
+        torch.cuda.synchronize()
+        ms = ev[0].elapsed_time(ev[1])
+    out["pinned_batch_encode"] = {"groups": G, "ms": round(ms, 3),
+                                  "GiBps": round(G * (k + m) * B / (ms * 1e-3) / 2**30, 2),
+                                  "note": "H2D data + encode + D2H recovery, serial on one stream"}
+    return out
 
 
 def pmc_traffic(sh, mode, k, m, B, G, e):
@@ -298,6 +356,11 @@ def main():
         }
         if root_res is not None:
             line["root_resident"] = root_res
+        if args.host_calls > 0 and world == 1:
+            try:
+                line["host_path"] = host_path(args, sh, torch, k, m, B, s)
+            except Exception as exc:  # a side measurement never loses the main line
+                line["host_path"] = {"error": f"{type(exc).__name__}: {exc}"}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
