@@ -30,6 +30,7 @@ EXPORTED_SYMBOLS = [
     "cauchy_256_default_stream", "cauchy_256_sync", "cauchy_256_profile", "cauchy_256_profile_read",
     "gf256_init_", "gf256_add_mem", "gf256_add2_mem", "gf256_addset_mem", "gf256_mul_mem",
     "gf256_muladd_mem", "gf256_memswap",
+    "shorthair_recovery_packet_bytes", "shorthair_encode_groups", "shorthair_recover_groups",
 ]
 
 if not os.path.exists(LIB_PATH):

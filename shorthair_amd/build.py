@@ -12,7 +12,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, os.environ.get("SH_LIB_NAME", "libcauchy256.so"))
-SOURCES = ["kernels.hip", "stageb.hip", "fixed_dispatch.cpp", "cauchy_256_host.cpp"]
+SOURCES = ["kernels.hip", "stageb.hip", "fixed_dispatch.cpp", "cauchy_256_host.cpp", "shorthair_groups.cpp"]
 HOST_SOURCES = ["gf256_host.cpp"]  # plain host C++ (no HIP): compiled with the host compiler
 CXX = os.environ.get("CXX", "g++")
 GEN_DIR = os.path.join(CSRC, os.environ.get("SH_GEN_DIR", "gen"))

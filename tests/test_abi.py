@@ -17,7 +17,7 @@ def _declared_functions():
     for h in os.listdir(INCLUDE):
         text = open(os.path.join(INCLUDE, h)).read()
         text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
-        for m in re.finditer(r"^\s*(?:extern\s+)?[\w\s\*]+?\b(\w+)\s*\([^;{]*\)\s*;", text, re.M):
+        for m in re.finditer(r"^\s*(?!\s*typedef\b)(?:extern\s+)?[\w\s\*]+?\b(\w+)\s*\([^;{]*\)\s*;", text, re.M):
             names.add(m.group(1))
     return names
 
