@@ -42,6 +42,8 @@ __device__ __forceinline__ uint32_t ldw_b(const uint8_t *p) {
                  : [tg] "s"(target), "{v[100:115]}"(t0), "{v[116:131]}"(t1)                      \
                  : "s40", "s41")
 
+static_assert(SH_SNIPA_ACC == 32 && SH_SNIPA_T0 == 96 && SH_SNIPA_T1 == 112,
+              "accumulating-snippet registers must match the asm constraints");
 static_assert(SH_SNIP_T0 == 100 && SH_SNIP_T1 == 116 && SH_SNIP_TMP == 132,
               "snippet registers must match the call constraints");
 
@@ -374,7 +376,7 @@ __global__ __launch_bounds__(256, 3) void stageb_acc(StageBArgs a) {
     const uint8_t *rd = lds + 4 * lane;
     const uint8_t *cf = lcoef + j0;
 
-    // accumulators pinned to v[64:127] (output j at v[64+8j..]), window tables to v[128:159]
+    // accumulators pinned to v[32:95] (output j at v[32+8j..]), window tables to v[96:127]
     u32x16 a01, a23, a45, a67;
 #pragma unroll
     for (int i = 0; i < 16; ++i) a01[i] = a23[i] = a45[i] = a67[i] = 0;
@@ -425,8 +427,8 @@ __global__ __launch_bounds__(256, 3) void stageb_acc(StageBArgs a) {
                 SH_GI_IDX("56")
                 SH_CALLX(g7)
                 SH_GI_OFF
-                : "+{v[64:79]}"(a01), "+{v[80:95]}"(a23), "+{v[96:111]}"(a45), "+{v[112:127]}"(a67)
-                : "{v[128:143]}"(t0), "{v[144:159]}"(t1), [g0] "s"(tg[0]), [g1] "s"(tg[1]),
+                : "+{v[32:47]}"(a01), "+{v[48:63]}"(a23), "+{v[64:79]}"(a45), "+{v[80:95]}"(a67)
+                : "{v[96:111]}"(t0), "{v[112:127]}"(t1), [g0] "s"(tg[0]), [g1] "s"(tg[1]),
                   [g2] "s"(tg[2]), [g3] "s"(tg[3]), [g4] "s"(tg[4]), [g5] "s"(tg[5]), [g6] "s"(tg[6]),
                   [g7] "s"(tg[7])
                 : "s40", "s41", "m0", "memory");

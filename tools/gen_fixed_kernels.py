@@ -31,6 +31,7 @@ CONFIGS = [(200, 32), (64, 16), (28, 4), (112, 16), (224, 32)]
 if os.environ.get("SH_CONFIGS"):  # experiments: e.g. SH_CONFIGS="200,32;64,16"
     CONFIGS = [tuple(map(int, c.split(","))) for c in os.environ["SH_CONFIGS"].split(";")]
 ROWS_PER_PART = int(os.environ.get("SH_ROWS_PER_PART", "8"))
+READ_PIN = os.environ.get("SH_READ_PIN", "0") == "1"
 
 
 def gf_tables():
@@ -154,6 +155,10 @@ class Body:
                         if nxt_issue < k:
                             L.append(f"    pre = src.pre({nxt_issue});")
                 L.append(f"    src.read({(x + 1) % R}, " + ", ".join(f"{nxt}{a}" for a in range(8)) + ");")
+                if READ_PIN:
+                    # keep the next block's ds_reads at the top of the step: left free, the
+                    # scheduler sinks them to ~25 VALU before their use (LDS latency exposed)
+                    L.append("    __builtin_amdgcn_sched_barrier(0);")
             L.append("    {")
             have = set()
             # Updates ordered by the high-half table entry: each T1 entry is built right before
@@ -284,7 +289,8 @@ def gen_config(k, m):
 # returns with s_setpc_b64. 256 snippets x 64 B = 16 KB, emitted inside the kernel behind an
 # s_branch (file-scope asm is dropped by HIP device compilation).
 SNIP_T0, SNIP_T1, SNIP_TMP = 100, 116, 132
-SNIPA_ACC, SNIPA_T0, SNIPA_T1 = 64, 128, 144
+# pinned low (v[32:127]) so a stage-B kernel fits 128 VGPRs (4 waves per SIMD)
+SNIPA_ACC, SNIPA_T0, SNIPA_T1 = 32, 96, 112
 
 
 def gen_snippets():
