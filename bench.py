@@ -20,7 +20,6 @@ import argparse
 import json
 import os
 import sys
-import threading
 import time
 
 import numpy as np
@@ -41,66 +40,105 @@ def parse():
     p.add_argument("--block", type=int, default=1400)
     p.add_argument("--groups", type=int, default=8192, help="code groups per GPU per op")
     p.add_argument("--erasures", type=int, default=32, help="erasures per decoded group (0=random 1..m)")
-    p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline sample wall time")
-    p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    p.add_argument("--cpu-seconds", type=float, default=4.0, help="CPU baseline: seconds per mode")
+    p.add_argument("--cpu-threads", type=int, default=0, help="0 = all host cores of this job")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--host-calls", type=int, default=50, help="single-group ABI calls timed (0 = skip)")
     p.add_argument("--host-groups", type=int, default=1024, help="groups of the pinned-host batch leg")
     p.add_argument("--root-steps", type=int, default=3,
                    help="N>1: steps of the root-resident variant (RCCL scatter -> encode -> gather); 0 = skip")
+    p.add_argument("--no-sweep", action="store_true", help="skip the C2/C3/C4/Tester-shape leg")
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher check without a GPU: ranks join a gloo group and rank 0 reports them")
     return p.parse_args()
 
 
-def cpu_baseline(k, m, B, e_fixed, seconds, threads):
-    """Reference codec (oracle/_ref/libref_cauchy.so) encode+decode on host threads.
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
 
-    Returns None when the reference build is absent. Each thread loops over a few distinct
-    groups (same synthetic generator as the GPU run) until `seconds` elapse.
-    """
+
+def launch(args):
+    """`--gpus N` outside a launcher: start N rank processes of this script (one per GPU, rank r on
+    device r) with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, and wait for
+    them. The parent never touches the GPU (it does not even import torch); rank 0 prints the
+    JSON line. Returns the first non-zero rank exit code."""
+    import subprocess
+    port = str(free_port())
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return next((rc for rc in rcs if rc != 0), 0)
+
+
+def dry_run(args, rank, world, local):
+    """Launcher check (no GPU): every rank joins a gloo group over 127.0.0.1 and rank 0 prints
+    what each rank saw."""
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        os.environ.update(RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
+    dist.init_process_group("gloo")
+    me = torch.tensor([rank, local, world, int(os.environ.get("MASTER_PORT", "0")), os.getpid()])
+    allr = [torch.zeros_like(me) for _ in range(dist.get_world_size())]
+    dist.all_gather(allr, me)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": dist.get_world_size(), "gpus_arg": args.gpus,
+                          "ranks": [dict(zip(("rank", "local_rank", "world_size", "master_port", "pid"),
+                                             [int(v) for v in t])) for t in allr]}), flush=True)
+    dist.destroy_process_group()
+
+
+def host_cores():
+    """CPUs this process may use (the GPU box gives each job a share of a large host: the
+    affinity mask / OMP_NUM_THREADS, not os.cpu_count(), says how many)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
+
+
+def cpu_model():
     try:
-        from oracle import pyoracle as po  # test infrastructure: the CPU baseline leg only
-        ref = po.reference()
-    except Exception:
-        ref = None
-    kind = "reference"
-    if ref is None:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(k, m, B, e_fixed, seconds, threads):
+    """The reference codec (oracle/_ref/libref_cauchy.so, compiled from catid/shorthair by
+    oracle/Makefile) timed by the native pthreads harness oracle/_ref/cpu_bench on this host:
+    1 thread and `threads` threads, as shipped (gf256_init not called) and after gf256_init()
+    (AVX2 XOR helpers). Same synthetic inputs as the GPU run. `value` is the fastest mode at
+    `threads` threads. Returns None when the harness is absent."""
+    import subprocess
+    exe = os.path.join(ROOT, "oracle", "_ref", "cpu_bench")
+    if not os.path.exists(exe):
         return None
-    ora = po.oracle()
-    nsample = 4
-    groups = []
-    for g in range(nsample):
-        data = po.fill_group(g, k, B, 0xBE)
-        _, rec = ora.encode(k, m, data, B)
-        e, rows = po.erasure_pattern(g, k, m, 0xBE, e_fixed)
-        whole = np.concatenate([data, rec])
-        groups.append((data, rows, whole, e))
-    counts = [0] * threads
-    bytes_done = [0] * threads
-    stop = time.perf_counter() + seconds
-
-    def work(t):
-        out = np.empty((m, B), np.uint8)
-        i = t
-        while time.perf_counter() < stop:
-            data, rows, whole, e = groups[i % nsample]
-            ref.encode(k, m, data, B, out)
-            blocks = [whole[r].copy() for r in rows]
-            ref.decode(k, m, blocks, [int(r) for r in rows], B)
-            counts[t] += 1
-            bytes_done[t] += (k + m) * B + (k + e) * B
-            i += threads
-
-    t0 = time.perf_counter()
-    ths = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
-    for th in ths:
-        th.start()
-    for th in ths:
-        th.join()
-    dt = time.perf_counter() - t0
-    return dict(value=round(sum(bytes_done) / dt / 2**30, 4), unit="GiB/s", cores=threads, kind=kind,
-                sample=f"{sum(counts)} encode+decode group pairs (k={k} m={m} B={B} e={e_fixed or 'rand'}) "
-                       f"over {dt:.1f}s on {threads} host threads, ctypes-released GIL, "
-                       f"reference built -O3 -march=x86-64-v3, gf256_init not called (as shipped)")
+    modes = {}
+    for t in sorted({1, threads}):
+        for mode in ("shipped", "init"):
+            r = subprocess.run([exe, str(k), str(m), str(B), str(e_fixed or m), str(t), str(seconds), mode],
+                               capture_output=True, text=True, timeout=seconds * 4 + 60)
+            if r.returncode != 0:
+                return None
+            kv = dict(x.split("=") for x in r.stdout.split())
+            modes[f"{mode}_t{t}"] = {"GiBps": float(kv["GiBps"]), "groups": int(kv["groups"]),
+                                     "us_per_encode": float(kv["us_per_encode"]),
+                                     "us_per_decode": float(kv["us_per_decode"])}
+    best = max((modes[f"{md}_t{threads}"]["GiBps"], md) for md in ("shipped", "init"))
+    return dict(value=round(best[0], 4), unit="GiB/s", cores=threads, kind="reference",
+                sample=f"native pthreads harness (oracle/cpu_bench.c), {seconds:g}s per mode, encode+decode "
+                       f"group pairs k={k} m={m} B={B} e={e_fixed or m}, reference built -O3 -march=x86-64-v3; "
+                       f"value = {best[1]} at {threads} threads",
+                cpu=cpu_model(), modes=modes)
 
 
 def root_resident(args, sh, shd, dist, torch, rank, world, G, k, m, B, s, enc_in, enc_out):
@@ -239,6 +277,80 @@ def packet_groups(args, k, m, B):
                     "recover: decode only (no delivery callback) in the timed loop"}
 
 
+# BASELINE.json config 2 (C2), config 4 (C4 sweep: k+m in {32,128,256} x B in {256,1400,64KiB},
+# m = (k+m)/8 as SURVEY §8d suggests) and the shapes catid/shorthair's Tester actually issues
+# (Shorthair.cpp:502-504 clamps m to 256-k).
+SWEEP = [("C2", 64, 16, 1400)] + [("C4", k, m, B) for (k, m) in ((28, 4), (112, 16), (224, 32))
+                                  for B in (256, 1400, 65536)] + \
+        [("tester", 200, 56, 1352), ("tester", 190, 66, 1336), ("tester", 190, 66, 1344)]
+
+
+def sweep(args, sh, torch, s):
+    """Per-shape device time of encode and decode (e = m worst case) with algorithmic GB/s and
+    fraction of the HBM peak, ~1.5 GB of input per op; plus C3 (random e in 1..32)."""
+    out = []
+    for tag, k, m, B in SWEEP:
+        G = max(8, int(1.5e9 // (k * B)))
+        data = torch.empty((G, k, B), dtype=torch.uint8, device="cuda")
+        rec = torch.empty((G, m, B), dtype=torch.uint8, device="cuda")
+        sh.fill_synthetic(data, k, B, G, 0, 0x5E, s)
+        r = {"config": tag, "k": k, "m": m, "B": B, "groups": G, "path": "fixed" if sh.has_fixed(k, m, B) else "generic"}
+        r.update(_time_ops(args, sh, torch, s, k, m, B, G, data, rec, min(k, m)))
+        out.append(r)
+        del data, rec
+    # C3: 8192 groups (200, 32, 1400), random erasure counts 1..32 (decode only)
+    k, m, B, G = 200, 32, 1400, 8192
+    data = torch.empty((G, k, B), dtype=torch.uint8, device="cuda")
+    rec = torch.empty((G, m, B), dtype=torch.uint8, device="cuda")
+    sh.fill_synthetic(data, k, B, G, 0, 0x5E, s)
+    r = {"config": "C3 random e", "k": k, "m": m, "B": B, "groups": G, "path": "fixed"}
+    r.update(_time_ops(args, sh, torch, s, k, m, B, G, data, rec, 0, encode=False))
+    out.append(r)
+    return out
+
+
+def _time_ops(args, sh, torch, s, k, m, B, G, data, rec, e_fixed, encode=True, iters=5):
+    sh.encode_batch(k, m, B, G, data, rec, s)
+    rows = np.zeros((G, k), np.uint8)
+    es = np.zeros(G, np.int64)
+    for g in range(G):
+        es[g], rows[g] = sh.erasure_pattern(g, k, m, 0x5E, e_fixed)
+    d_rows = torch.from_numpy(rows).cuda()
+    whole = torch.cat([data, rec], dim=1)
+    blocks = whole[torch.arange(G, device="cuda")[:, None], d_rows.long()]
+    del whole
+    emax = min(k, m)
+    out = torch.empty((G, emax, B), dtype=torch.uint8, device="cuda")
+    orow = torch.empty((G, emax), dtype=torch.uint8, device="cuda")
+    ocnt = torch.empty(G, dtype=torch.int32, device="cuda")
+    sh.batch_reserve(k, m, B, G)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    te = td = 0.0
+    for it in range(iters + 1):
+        ev[0].record()
+        if encode:
+            assert sh.encode_batch(k, m, B, G, data, rec, s) == 0
+        ev[1].record()
+        assert sh.decode_batch_out(k, m, B, G, blocks, d_rows, out, orow, ocnt, s) == 0
+        ev[2].record()
+        torch.cuda.synchronize()
+        if it:  # first pass warms up
+            te += ev[0].elapsed_time(ev[1]) / iters
+            td += ev[1].elapsed_time(ev[2]) / iters
+    g_chk = torch.arange(G, device="cuda")[:, None]
+    ok = bool(torch.equal(ocnt.cpu(), torch.from_numpy(es).int()))
+    if ok and e_fixed == emax:
+        ok = bool(torch.equal(out, data[g_chk, orow.long()]))
+    enc_b, dec_b = G * (k + m) * B, int((k + es).sum()) * B
+    r = {"decode_ms": round(td, 4), "decode_GBps": round(dec_b / td / 1e6, 1),
+         "decode_frac": round(dec_b / td / 1e-3 / HBM_PEAK, 4), "mean_e": round(float(es.mean()), 2),
+         "decode_ok": ok}
+    if encode:
+        r.update({"encode_ms": round(te, 4), "encode_GBps": round(enc_b / te / 1e6, 1),
+                  "encode_frac": round(enc_b / te / 1e-3 / HBM_PEAK, 4)})
+    return r
+
+
 def pmc_traffic(sh, mode, k, m, B, G, e):
     """HBM bytes per launch of the dominant kernel from the committed PMC summary
     (profiles/*/traffic*.json, written by tools/gpu_traffic.sh: FETCH_SIZE and WRITE_SIZE in
@@ -265,15 +377,20 @@ def pmc_traffic(sh, mode, k, m, B, G, e):
 
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args))  # before anything touches the GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, rank, world, local)
+    import torch
+    import torch.distributed as dist
+
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()
     else:
         torch.cuda.set_device(0)
     import shorthair_amd as sh
@@ -373,7 +490,7 @@ def main():
         dom = (("encode kernel", enc_ms) if not (a_ms > enc_ms) else ("decode stage-A kernel", a_ms))
         traffic, traffic_src = pmc_traffic(sh, "enc" if dom[0].startswith("encode") else "dec", k, m, B, G,
                                            args.erasures)
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        threads = args.cpu_threads or host_cores()
         cpu = None if args.no_cpu else cpu_baseline(k, m, B, args.erasures, args.cpu_seconds, threads)
         line = {
             "metric": "cauchy_256 encode+decode GiB/s (device-resident), k=200 m=32 ×1400B; %HBM peak",
@@ -407,6 +524,11 @@ def main():
         }
         if root_res is not None:
             line["root_resident"] = root_res
+        if not args.no_sweep and world == 1:
+            try:
+                line["sweep"] = sweep(args, sh, torch, s)
+            except Exception as exc:  # a side measurement never loses the main line
+                line["sweep"] = {"error": f"{type(exc).__name__}: {exc}"}
         if args.host_calls > 0 and world == 1:
             try:
                 line["host_path"] = host_path(args, sh, torch, k, m, B, s)

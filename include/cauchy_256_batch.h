@@ -46,8 +46,19 @@ int cauchy_256_decode_batch_out(int k, int m, int block_bytes, int groups, const
                                 const unsigned char *d_rows, void *d_out, unsigned char *d_out_rows,
                                 int *d_out_count, void *stream);
 
-/* Pre-allocate the internal decode workspace so later calls allocate nothing (graph capture). */
+/* Pre-allocate the internal decode workspace so later calls allocate nothing (graph capture).
+ * Workspaces are per stream (decodes in flight on different streams never share scratch):
+ * cauchy_256_batch_reserve sizes the null stream's workspace and the minimum size of every
+ * workspace created later; cauchy_256_batch_reserve_stream does the same for `stream`. */
 int cauchy_256_batch_reserve(int k, int m, int block_bytes, int groups);
+int cauchy_256_batch_reserve_stream(int k, int m, int block_bytes, int groups, void *stream);
+
+/* Malformed decode groups (more recovery blocks than erased originals: duplicate rows, outside
+ * the reference's contract) are left untouched, counted, and flagged with d_out_count[g] = -1 by
+ * cauchy_256_decode_batch_out. This waits for `stream` and returns the number of such groups
+ * since the previous call (resetting the count), or -2 on a GPU error. The single-group
+ * cauchy_256_decode returns -1 for such a group. */
+int cauchy_256_batch_errors(void *stream);
 
 /* Synthetic workload: block x of group g0+g = PCG32 Seed((g0+g)*256 + x, cfg) words (the same
  * stream as the test oracle), written to d_out[groups][n][block_bytes]. */
@@ -60,6 +71,10 @@ int cauchy_256_fill_synthetic(void *d_out, int n, int block_bytes, int groups,
  * Returns e, or -1 on bad arguments. */
 int cauchy_256_erasure_pattern(unsigned long long g, int k, int m, unsigned long long cfg, int e_fixed,
                                unsigned char *rows_out);
+
+/* Which kernels code (k, m, block_bytes): 1 = compile-time-scheduled (generated for this (k, m)),
+ * 0 = the generic runtime-coefficient kernels, -1 = invalid parameters. Host only. */
+int cauchy_256_batch_path(int k, int m, int block_bytes);
 
 /* The library's private stream (used by the single-group calls) and a synchronize helper for
  * callers without HIP. */

@@ -14,7 +14,7 @@ import os
 
 __all__ = ["lib", "Block", "CAUCHY_256_VERSION", "cauchy_256_init", "cauchy_256_encode",
            "cauchy_256_decode", "encode_batch", "decode_batch", "decode_batch_out",
-           "fill_synthetic", "erasure_pattern", "batch_reserve", "default_stream", "sync", "LIB_PATH",
+           "fill_synthetic", "erasure_pattern", "batch_reserve", "batch_errors", "has_fixed", "default_stream", "sync", "LIB_PATH",
            "EXPORTED_SYMBOLS"]
 
 CAUCHY_256_VERSION = 2
@@ -25,7 +25,8 @@ LIB_PATH = os.environ.get("SH_LIB_PATH") or os.path.join(os.path.dirname(os.path
 EXPORTED_SYMBOLS = [
     "_cauchy_256_init", "cauchy_256_encode", "cauchy_256_decode",
     "cauchy_256_batch_init", "cauchy_256_encode_batch", "cauchy_256_decode_batch",
-    "cauchy_256_decode_batch_out", "cauchy_256_batch_reserve", "cauchy_256_fill_synthetic",
+    "cauchy_256_decode_batch_out", "cauchy_256_batch_reserve", "cauchy_256_batch_reserve_stream",
+    "cauchy_256_batch_errors", "cauchy_256_batch_path", "cauchy_256_fill_synthetic",
     "cauchy_256_erasure_pattern",
     "cauchy_256_default_stream", "cauchy_256_sync", "cauchy_256_profile", "cauchy_256_profile_read",
     "gf256_init_", "gf256_add_mem", "gf256_add2_mem", "gf256_addset_mem", "gf256_mul_mem",
@@ -62,6 +63,12 @@ lib.cauchy_256_decode_batch_out.argtypes = [_c.c_int] * 4 + [_c.c_void_p] * 6
 lib.cauchy_256_decode_batch_out.restype = _c.c_int
 lib.cauchy_256_batch_reserve.argtypes = [_c.c_int] * 4
 lib.cauchy_256_batch_reserve.restype = _c.c_int
+lib.cauchy_256_batch_reserve_stream.argtypes = [_c.c_int] * 4 + [_c.c_void_p]
+lib.cauchy_256_batch_reserve_stream.restype = _c.c_int
+lib.cauchy_256_batch_errors.argtypes = [_c.c_void_p]
+lib.cauchy_256_batch_errors.restype = _c.c_int
+lib.cauchy_256_batch_path.argtypes = [_c.c_int] * 3
+lib.cauchy_256_batch_path.restype = _c.c_int
 lib.cauchy_256_fill_synthetic.argtypes = [_c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
                                           _c.c_ulonglong, _c.c_ulonglong, _c.c_void_p]
 lib.cauchy_256_fill_synthetic.restype = _c.c_int
@@ -155,6 +162,16 @@ def erasure_pattern(g, k, m, cfg, e_fixed=0):
 
 def batch_reserve(k, m, block_bytes, groups):
     return _check(lib.cauchy_256_batch_reserve(k, m, block_bytes, groups), "batch_reserve")
+
+
+def batch_errors(stream=None):
+    """Malformed decode groups since the last call (waits for the stream)."""
+    return _check(lib.cauchy_256_batch_errors(_stream(stream)), "batch_errors")
+
+
+def has_fixed(k, m, block_bytes):
+    """True when (k, m, block_bytes) runs on compile-time-scheduled kernels."""
+    return lib.cauchy_256_batch_path(k, m, block_bytes) == 1
 
 
 def default_stream():

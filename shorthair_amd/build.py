@@ -53,14 +53,20 @@ FLAGS += os.environ.get("SH_EXTRA_FLAGS", "").split()  # experiments only (tools
 OBJ_DIR = os.path.join(HERE, os.environ.get("SH_OBJ_DIR", "build_obj"))
 
 
+def _headers():
+    """Every header a source can include: csrc/*.h*, the generated headers/.inc files, include/*.
+    (Conservative: any header change recompiles every object.)"""
+    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".hpp"))]
+    hs += [os.path.join(GEN_DIR, f) for f in os.listdir(GEN_DIR) if f.endswith((".h", ".inc"))]
+    inc = os.path.join(HERE, "..", "include")
+    hs += [os.path.join(inc, f) for f in os.listdir(inc)]
+    return hs
+
+
 def _compile(src, verbose):
     obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(
-            os.path.getmtime(src), os.path.getmtime(os.path.join(CSRC, "fixed_common.hpp")),
-            *( [os.path.getmtime(src[:-8] + ".inc")] if src.endswith(("_enc.hip", "_dec.hip")) else []),
-            os.path.getmtime(os.path.join(CSRC, "kernels.hpp")),
-            *[os.path.getmtime(os.path.join(HERE, "..", "include", h))
-              for h in os.listdir(os.path.join(HERE, "..", "include"))]):
+            os.path.getmtime(src), *[os.path.getmtime(h) for h in _headers()]):
         return obj, None
     if os.path.basename(src) in HOST_SOURCES:
         cmd = [CXX, "-O3", "-std=c++17", "-fPIC", "-Wall", "-c", src, "-o", obj]

@@ -38,13 +38,17 @@ using sh::Geometry;
 
 inline int round4(int x) { return (x + 3) & ~3; }
 
-// Grow-only device buffer.
+// Grow-only device buffer. `owner` (if any) is the only stream that uses it: growing waits for
+// that stream before freeing the old allocation.
 struct DevBuf {
     void *p = nullptr;
     size_t n = 0;
-    int ensure(size_t bytes) {
+    int ensure(size_t bytes, hipStream_t owner = nullptr) {
         if (bytes <= n) return 0;
-        if (p) (void)hipFree(p);
+        if (p) {
+            (void)hipStreamSynchronize(owner);
+            (void)hipFree(p);
+        }
         p = nullptr;
         n = 0;
         if (hipMalloc(&p, bytes) != hipSuccess) {
@@ -74,10 +78,12 @@ struct PinnedBuf {
 };
 
 struct Context {
-    std::mutex mu;          // guards lazy state (tables, caches, workspace, staging)
+    std::mutex mu;          // guards lazy state (tables, caches, workspaces, profiling events)
     bool ready = false;
     int device = 0;
     hipStream_t stream = nullptr;
+    uint64_t snip_base = 0;           // stage-B snippet table address (code object)
+    int *d_errors = nullptr;          // malformed-group counter (decode setup)
     uint64_t *d_rowbytes = nullptr;   // 256 x 8 bytes
     uint8_t *d_exp = nullptr;         // 512
     uint16_t *d_log = nullptr;        // 256
@@ -85,7 +91,10 @@ struct Context {
     // followed by the raw (m-1) x k rows 1..m-1 and the Cauchy parameters X'[k], Y'[m] for
     // decode setup.
     std::map<std::pair<int, int>, uint8_t *> gens;
-    DevBuf ws;                        // decode workspace
+    // Decode workspace per stream: two decodes in flight on different streams never share
+    // scratch; calls on one stream are ordered by the stream itself.
+    std::map<hipStream_t, DevBuf> ws;
+    size_t ws_reserve = 0;            // cauchy_256_batch_reserve: minimum size of a new workspace
     // stage timing (cauchy_256_profile): per profiled decode, events around setup / stage A /
     // stage B, in a ring of `evq.size()` quadruples (no host synchronisation while recording)
     std::vector<std::array<hipEvent_t, 4>> evq;
@@ -124,14 +133,32 @@ int init_locked(Context &c, int device) {
     SH_CHECK(hipMemcpy(c.d_exp, f.exp, 512, hipMemcpyHostToDevice));
     SH_CHECK(hipMalloc(&c.d_log, 512));
     SH_CHECK(hipMemcpy(c.d_log, f.log, 512, hipMemcpyHostToDevice));
+    SH_CHECK(hipMalloc(&c.d_errors, sizeof(int)));
+    SH_CHECK(hipMemset(c.d_errors, 0, sizeof(int)));
+    SH_CHECK(sh::stageb_snip_base(&c.snip_base, c.stream));
     c.device = device;
     c.ready = true;
     return 0;
 }
 
+// Every entry point runs on the library's device, whatever the calling thread had current
+// (HIP's current device is per thread; allocations and launches follow it).
 int ensure_init(Context &c) {
+    {
+        std::lock_guard<std::mutex> g(c.mu);
+        if (int rc = init_locked(c, c.device)) return rc;
+    }
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != c.device) SH_CHECK(hipSetDevice(c.device));
+    return 0;
+}
+
+// Workspace of `stream`, grown to at least `bytes` (under c.mu).
+uint8_t *workspace(Context &c, hipStream_t stream, size_t bytes) {
     std::lock_guard<std::mutex> g(c.mu);
-    return init_locked(c, c.device);
+    DevBuf &b = c.ws[stream];
+    if (b.ensure(std::max(bytes, c.ws_reserve), stream)) return nullptr;
+    return static_cast<uint8_t *>(b.p);
 }
 
 // Device generator for (k, m), m >= 2, k + m <= 256. Cached; created once per shape.
@@ -176,33 +203,7 @@ hipError_t launch_fixed_batch(int k, int m, int B, int groups, const uint8_t *in
     a.geo = sh::make_geometry(B);
     a.pos = pos;
     a.rpos = rpos;
-    if (!std::getenv("SH_DEBUG_STAMPS")) return sh::launch_fixed(k, m, a, dec, s);
-    // Diagnostic (library built with -DSH_EXPERIMENT_STAMPS): per-wave cycle stamps -> stderr.
-    const size_t nw = static_cast<size_t>(groups) * B / 8 / 4 + 4096;  // >= waves of any shape
-    unsigned long long *d = nullptr;
-    if (hipMalloc(&d, nw * 4 * 8) != hipSuccess) return hipErrorOutOfMemory;
-    hipMemsetAsync(d, 0, nw * 4 * 8, s);
-    a.dbg = d;
-    hipError_t e = sh::launch_fixed(k, m, a, dec, s);
-    std::vector<unsigned long long> h(nw * 4);
-    hipMemcpyAsync(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost, s);
-    hipStreamSynchronize(s);
-    hipFree(d);
-    double vm = 0, bar = 0, life = 0;
-    unsigned long long t0 = ~0ull, t1 = 0;
-    size_t n = 0;
-    for (size_t i = 0; i < nw; ++i) {
-        if (h[i * 4 + 3] == 0) continue;
-        ++n;
-        vm += h[i * 4];
-        bar += h[i * 4 + 1];
-        life += h[i * 4 + 3] - h[i * 4 + 2];
-        t0 = std::min(t0, h[i * 4 + 2]);
-        t1 = std::max(t1, h[i * 4 + 3]);
-    }
-    std::fprintf(stderr, "stamps %s: waves %zu, mean wave life %.0f, vmcnt wait %.1f%%, barrier %.1f%%, span %llu\n",
-                 dec ? "dec" : "enc", n, life / n, 100 * vm / life, 100 * bar / life, t1 - t0);
-    return e;
+    return sh::launch_fixed(k, m, a, dec, s);
 }
 
 // ---- batched encode ----
@@ -252,21 +253,23 @@ int encode_batch(int k, int m, int B, int groups, const uint8_t *d_in, uint8_t *
 
 // Workspace carve for decode of `groups` groups.
 struct DecodeWS {
-    bool fixed;       // stage A by a compile-time-scheduled kernel (has_fixed(k, m, B))
+    bool fixed;       // stage A by a compile-time-scheduled kernel, stage B by stageb_fixed
     int emax, ldA, ldB, nres;  // nres: residual rows per group (m when fixed, else emax)
     int *e;
-    uint8_t *rec_idx, *erasures, *coefA, *coefB, *residual, *recovered, *pos, *rpos;
+    uint8_t *rec_idx, *erasures, *coefA, *coefB, *residual, *recovered, *pos, *rpos, *rrow;
+    uint64_t *targets;
     long long coefA_gs, coefB_gs;
 };
 
 size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool need_recovered) {
-    w.fixed = sh::has_fixed(k, m, B);
+    const sh::Geometry geo = sh::make_geometry(B);
     w.emax = std::min(k, m);
+    w.fixed = sh::has_fixed(k, m, B) && sh::stageb_fixed_ok(geo, w.emax);
     w.ldA = w.fixed ? 0 : round4(k);
-    w.ldB = (w.emax + 7) & ~7;  // stage-B coefficients [n_in][ldB] (transposed, 8-byte rows)
+    w.ldB = (w.emax + 7) & ~7;  // stage-B coefficients [i][ldB] (transposed, 8-entry rows)
     w.nres = w.fixed ? m : w.emax;
     w.coefA_gs = static_cast<long long>(w.emax) * w.ldA;
-    w.coefB_gs = static_cast<long long>(w.nres) * w.ldB;
+    w.coefB_gs = static_cast<long long>(w.emax) * w.ldB;
     size_t off = 0;
     auto take = [&](size_t bytes) {
         uint8_t *p = base ? base + off : nullptr;
@@ -278,7 +281,9 @@ size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool n
     w.rec_idx = take(G * w.emax);
     w.erasures = take(G * w.emax);
     w.coefA = w.fixed ? nullptr : take(G * w.coefA_gs);
-    w.coefB = take(G * w.coefB_gs);
+    w.coefB = w.fixed ? nullptr : take(G * w.coefB_gs);
+    w.targets = w.fixed ? reinterpret_cast<uint64_t *>(take(G * w.emax * w.ldB * sizeof(uint64_t))) : nullptr;
+    w.rrow = w.fixed ? take(G * w.emax) : nullptr;
     w.pos = w.fixed ? take(G * round4(k)) : nullptr;
     w.rpos = w.fixed ? take(G * round4(m)) : nullptr;
     w.residual = take(G * w.nres * static_cast<size_t>(B) + 256);  // + slack: word over-read
@@ -286,12 +291,25 @@ size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool n
     return off;
 }
 
-hipError_t launch_stage_b(Context &, const DecodeWS &w, int n_in, int B, int groups, uint8_t *dst,
-                          hipStream_t s) {
+hipError_t launch_stage_b(const DecodeWS &w, int n_in, int B, int groups, uint8_t *dst, hipStream_t s) {
+    if (w.fixed) {
+        sh::StageBFixedArgs f{};
+        f.in = w.residual;
+        f.in_gstride = static_cast<long long>(n_in) * B;
+        f.out = dst;
+        f.out_gstride = static_cast<long long>(w.emax) * B;
+        f.e = w.e;
+        f.rrow = w.rrow;
+        f.targets = w.targets;
+        f.emax = w.emax;
+        f.ldT = w.ldB;
+        f.groups = groups;
+        f.geo = sh::make_geometry(B);
+        return sh::launch_stageb_fixed(f, s);
+    }
     sh::StageBArgs b{};
     b.in = w.residual;
     b.in_gstride = static_cast<long long>(n_in) * B;
-    b.in_slack = 256;  // carve(): the residual carries 256 bytes of slack
     b.n_in = n_in;
     b.out = dst;
     b.out_gstride = static_cast<long long>(w.emax) * B;
@@ -301,34 +319,7 @@ hipError_t launch_stage_b(Context &, const DecodeWS &w, int n_in, int B, int gro
     b.ldT = w.ldB;
     b.groups = groups;
     b.geo = sh::make_geometry(B);
-    if (!std::getenv("SH_DEBUG_STAMPS")) return sh::launch_stageb(b, w.emax, s);
-    // Diagnostic (library built with -DSH_EXPERIMENT_STAMPS): per-wave phase stamps -> stderr.
-    const size_t nw = static_cast<size_t>(groups) * ((B / 8 / 4 + 63) / 64) * ((w.emax + 31) / 32) * 4;
-    unsigned long long *d = nullptr;
-    if (hipMalloc(&d, nw * 8 * 8) != hipSuccess) return hipErrorOutOfMemory;
-    hipMemsetAsync(d, 0, nw * 8 * 8, s);
-    b.dbg = d;
-    hipError_t e = sh::launch_stageb(b, w.emax, s);
-    std::vector<unsigned long long> h(nw * 8);
-    hipMemcpyAsync(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost, s);
-    hipStreamSynchronize(s);
-    hipFree(d);
-    double ph[5] = {0, 0, 0, 0, 0};
-    unsigned long long t0 = ~0ull, t1 = 0;
-    size_t n = 0;
-    for (size_t i = 0; i < nw; ++i) {
-        const unsigned long long *r = &h[i * 8];
-        if (r[5] == 0) continue;
-        ++n;
-        for (int j = 0; j < 5; ++j) ph[j] += static_cast<double>(r[j + 1] - r[j]);
-        t0 = std::min(t0, r[0]);
-        t1 = std::max(t1, r[5]);
-    }
-    std::fprintf(stderr,
-                 "stamps stageB: waves %zu, mean cycles: prologue %.0f, dma %.0f, rows %.0f, stores %.0f, "
-                 "drain %.0f; span %llu\n",
-                 n, ph[0] / n, ph[1] / n, ph[2] / n, ph[3] / n, ph[4] / n, t1 - t0);
-    return e;
+    return sh::launch_stageb(b, w.emax, s);
 }
 
 // Common decode core (m >= 2, valid params): writes recovered blocks densely into `dst`
@@ -359,10 +350,17 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
     sa.ldB = w.ldB;
     sa.pos = w.pos;
     sa.rpos = w.rpos;
+    sa.rrow = w.rrow;
+    sa.targets = w.targets;
+    sa.snip_base = c.snip_base;
+    sa.errors = c.d_errors;
     hipEvent_t *ev = nullptr;
-    if (!c.evq.empty()) {
+    {
         std::lock_guard<std::mutex> g(c.mu);
-        ev = c.evq[c.ev_next].data();
+        if (!c.evq.empty()) ev = c.evq[c.ev_next].data();
+    }
+    if (ev) {
+        std::lock_guard<std::mutex> g(c.mu);
         c.ev_next = (c.ev_next + 1) % static_cast<int>(c.evq.size());
         c.ev_count = std::min(c.ev_count + 1, static_cast<int>(c.evq.size()));
     }
@@ -378,7 +376,7 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
                                       w.residual, static_cast<long long>(m) * B, w.pos, w.rpos, true, s));
         if (ev) SH_CHECK(hipEventRecord(ev[2], s));
         // Stage B: recovered_j = sum_y M(S^-1[j][i(y)]) residual_y over the received rows y
-        SH_CHECK(launch_stage_b(c, w, m, B, groups, dst, s));
+        SH_CHECK(launch_stage_b(w, m, B, groups, dst, s));
         if (ev) SH_CHECK(hipEventRecord(ev[3], s));
         return 0;
     }
@@ -401,7 +399,7 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
     a.geo = geo;
     SH_CHECK(sh::launch_apply(a, true, s));
     // Stage B: recovered_j = sum_i M(S^-1[j][i]) residual_i
-    SH_CHECK(launch_stage_b(c, w, w.emax, B, groups, dst, s));
+    SH_CHECK(launch_stage_b(w, w.emax, B, groups, dst, s));
     return 0;
 }
 
@@ -429,12 +427,9 @@ int decode_batch(int k, int m, int B, int groups, uint8_t *d_blocks, uint8_t *d_
     }
     if (k + m > 256 || B % 8 != 0) return invalid_decode_status(k, groups, d_rows, s);
     DecodeWS w{};
-    const size_t need = carve(w, nullptr, k, m, B, groups, true);
-    {
-        std::lock_guard<std::mutex> g(c.mu);
-        if (int rc = c.ws.ensure(need)) return rc;
-        carve(w, static_cast<uint8_t *>(c.ws.p), k, m, B, groups, true);
-    }
+    uint8_t *wsp = workspace(c, s, carve(w, nullptr, k, m, B, groups, true));
+    if (!wsp) return -2;
+    carve(w, wsp, k, m, B, groups, true);
     if (int rc = decode_core(c, k, m, B, groups, d_blocks, d_rows, w, w.recovered, s)) return rc;
     sh::ScatterArgs sc{};
     sc.src = w.recovered;
@@ -486,12 +481,9 @@ extern "C" int cauchy_256_decode_batch_out(int k, int m, int block_bytes, int gr
     hipStream_t s = pick(stream);
     if (k + m > 256 || block_bytes % 8 != 0) return invalid_decode_status(k, groups, d_rows, s);
     DecodeWS w{};
-    const size_t need = carve(w, nullptr, k, m, block_bytes, groups, false);
-    {
-        std::lock_guard<std::mutex> g(c.mu);
-        if (int rc = c.ws.ensure(need)) return rc;
-        carve(w, static_cast<uint8_t *>(c.ws.p), k, m, block_bytes, groups, false);
-    }
+    uint8_t *wsp = workspace(c, s, carve(w, nullptr, k, m, block_bytes, groups, false));
+    if (!wsp) return -2;
+    carve(w, wsp, k, m, block_bytes, groups, false);
     if (int rc = decode_core(c, k, m, block_bytes, groups, static_cast<const uint8_t *>(d_blocks),
                              d_rows, w, static_cast<uint8_t *>(d_out), s))
         return rc;
@@ -503,14 +495,31 @@ extern "C" int cauchy_256_decode_batch_out(int k, int m, int block_bytes, int gr
 }
 
 extern "C" int cauchy_256_batch_reserve(int k, int m, int block_bytes, int groups) {
+    return cauchy_256_batch_reserve_stream(k, m, block_bytes, groups, nullptr);
+}
+
+extern "C" int cauchy_256_batch_reserve_stream(int k, int m, int block_bytes, int groups, void *stream) {
     Context &c = ctx();
     if (int rc = ensure_init(c)) return rc;
-    if (k < 2 || m < 2 || k + m > 256) return 0;
+    if (k < 2 || m < 2 || k + m > 256 || block_bytes <= 0 || groups <= 0) return 0;
     DecodeWS w{};
     const size_t need = carve(w, nullptr, k, m, block_bytes, groups, true);
     if (!generator(c, k, m)) return -2;
-    std::lock_guard<std::mutex> g(c.mu);
-    return c.ws.ensure(need);
+    {
+        std::lock_guard<std::mutex> g(c.mu);
+        c.ws_reserve = std::max(c.ws_reserve, need);
+    }
+    return workspace(c, pick(stream), need) ? 0 : -2;
+}
+
+extern "C" int cauchy_256_batch_errors(void *stream) {
+    Context &c = ctx();
+    if (int rc = ensure_init(c)) return rc;
+    SH_CHECK(hipStreamSynchronize(pick(stream)));
+    int n = 0;
+    SH_CHECK(hipMemcpy(&n, c.d_errors, sizeof(int), hipMemcpyDeviceToHost));
+    SH_CHECK(hipMemset(c.d_errors, 0, sizeof(int)));
+    return n;
 }
 
 extern "C" int cauchy_256_fill_synthetic(void *d_out, int n, int block_bytes, int groups,
@@ -560,6 +569,11 @@ extern "C" int cauchy_256_erasure_pattern(unsigned long long g, int k, int m, un
     for (int y = 0; y < m; ++y)
         if (used[y]) rows_out[n++] = static_cast<uint8_t>(k + y);
     return e;
+}
+
+extern "C" int cauchy_256_batch_path(int k, int m, int block_bytes) {
+    if (k < 1 || m < 1 || k + m > 256 || block_bytes <= 0 || block_bytes % 8 != 0) return -1;
+    return sh::has_fixed(k, m, block_bytes) ? 1 : 0;
 }
 
 extern "C" void *cauchy_256_default_stream(void) {
@@ -663,7 +677,17 @@ extern "C" int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes) {
     const int rc = decode_batch(k, m, block_bytes, 1, d, d + data_bytes, c.stream);
     if (rc != 0) return rc;
     SH_CHECK(hipMemcpyAsync(h, d, data_bytes + k, hipMemcpyDeviceToHost, c.stream));
+    int e = 0;
+    if (m >= 2 && k + m <= 256 && block_bytes % 8 == 0) {
+        // the decode core ran: the group's e is the first word of this stream's workspace (carve)
+        const uint8_t *wsp = workspace(c, c.stream, 0);
+        if (!wsp) return -2;
+        SH_CHECK(hipMemcpyAsync(&e, wsp, sizeof(int), hipMemcpyDeviceToHost, c.stream));
+    }
     SH_CHECK(hipStreamSynchronize(c.stream));
+    // A group with more recovery blocks than erasures (outside the reference's contract: its
+    // rows would be duplicates) is left untouched and reported as invalid.
+    if (e < 0) return -1;
     // Write back only what the codec may change: the blocks whose row was >= k (they receive
     // recovered data) -- originals are never modified (reference row contract).
     for (int i = 0; i < k; ++i) {

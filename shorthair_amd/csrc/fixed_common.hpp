@@ -25,8 +25,8 @@
 // -- every wave's share of those slots has landed, and every wave is past block x-1, so the
 // slots of blocks <= x-1 are free and their DMAs (blocks up to x+R-1) are issued right there.
 // R >= 2S+1 keeps R-2S-1 blocks of DMA in flight beyond the group being waited for. Fewer
-// barriers matter: measured per-wave stamps (SH_EXPERIMENT_STAMPS) showed 41 % of a wave's
-// life at the barrier with S = 1; S = 4 is 6-8 % faster. All P part-waves read the same slots:
+// barriers matter: measured per-wave stamps (round 1) showed 41 % of a wave's life at the barrier
+// with S = 1; S = 4 is 6-8 % faster. All P part-waves read the same slots:
 // HBM sees each input byte once.
 //
 // Sub-block tails. When sub = B/8 is not a multiple of 4 (175 at B = 1400) the last 4-column
@@ -89,9 +89,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wg_rsrc(const uint8_t *base, l
 }
 
 // Compile-time shape of one kernel instance.
-template <int K_, int M_, int P_, int CW_, int R_>
+// DMA_ = false only in measurement builds (tools/gen_fixed_kernels.py SH_GEN_ABLATE=nodma).
+template <int K_, int M_, int P_, int CW_, int R_, bool DMA_ = true>
 struct Shape {
     static constexpr int K = K_, M = M_, P = P_, CW = CW_, R = R_, W = 16;
+    static constexpr bool DMA = DMA_;
     static constexpr int NW = CW * P, NT = 64 * NW, COLS = CW * 64;
     static constexpr int ROWB = COLS * 4;               // bytes of one sub-block row of a slot
     static constexpr int SLOT = 8 * ROWB;               // bytes per ring slot (one input block)
@@ -103,8 +105,9 @@ struct Shape {
 
 // Per-lane geometry shared by the source and the sink.
 struct WGInfo {
-    long long col0;  // first column of the workgroup
-    int g_first;     // group of col0 (descriptor base)
+    long long col0;  // first column of the tile (may precede lo: the first tile of odd workgroups)
+    long long lo, hi;  // this workgroup's columns [lo, hi): whole groups
+    int g_first;     // group of max(col0, lo) (descriptor base)
     int wave, lane, c;
     int gl, q;       // this lane's group (relative to g_first) and word column
     bool valid;      // g < groups
@@ -146,10 +149,10 @@ struct Src {
             const int aa = off / S::ROWB;
             const int cc = (off - aa * S::ROWB) / 4;
             const long long colx = w.col0 + cc;
-            const int gx = static_cast<int>(colx / geo.nq);
+            const int gx = colx >= 0 ? static_cast<int>(colx / geo.nq) : -1;
             const int qx = static_cast<int>(colx - static_cast<long long>(gx) * geo.nq);
             dgl[j] = gx - w.g_first;
-            dbase[j] = gx < a.groups
+            dbase[j] = (colx >= w.lo && colx < w.hi)
                            ? static_cast<uint32_t>(gx - w.g_first) * gstride + col_off(qx, geo) + aa * geo.sub
                            : OOR;
         }
@@ -157,29 +160,12 @@ struct Src {
 
     // Wait until this wave's DMAs of steps <= T are done (I = steps issued so far), then join the
     // workgroup barrier. One asm statement: nothing is scheduled between the two.
-#ifndef SH_EXPERIMENT_STAMPS
     template <int T, int I>
     __device__ __forceinline__ static void wait() {
         constexpr int N = (I - T - 1) * S::DPW;
         static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
         asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
     }
-#else  // diagnostic build: cycles spent in the vmcnt wait and in the barrier, per wave
-    mutable unsigned long long st_vm = 0, st_bar = 0, st_t0 = 0;
-    template <int T, int I>
-    __device__ __forceinline__ void wait() const {
-        constexpr int N = (I - T - 1) * S::DPW;
-        unsigned long long t0, t1, t2;
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
-        asm volatile("s_barrier" ::: "memory");
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t2)::"memory");
-        if (st_t0 == 0) st_t0 = t0;
-        st_vm += t1 - t0;
-        st_bar += t2 - t1;
-    }
-#endif
 
     // After the last step: every wave's reads of the ring are done before any wave writes its
     // store scratch (which aliases the ring).
@@ -201,9 +187,6 @@ struct Src {
 
     // DMA of input step x into its ring slot.
     __device__ __forceinline__ void issue(int x, const Pre &pr) const {
-#ifdef SH_EXPERIMENT_NO_DMA  // timing experiment only: compute on whatever the ring holds
-        return;
-#endif
         uint8_t *slot = const_cast<uint8_t *>(lds) + (x % S::R) * S::SLOT;
 #pragma unroll
         for (int j = 0; j < S::DPW; ++j) {
@@ -250,13 +233,14 @@ struct Src {
         lane = w.lane;
         const int t = w.lane & 15;
         const long long colx = w.col0 + (w.c - w.lane) + 4 * t;
-        const int gx = static_cast<int>(colx / geo.nq);
+        const int gx = colx >= 0 ? static_cast<int>(colx / geo.nq) : -1;
         const int qx = static_cast<int>(colx - static_cast<long long>(gx) * geo.nq);
-        cgl = gx - w.g_first;
+        const bool ok = colx >= w.lo && colx < w.hi;
+        cgl = ok ? gx - w.g_first : 0;
         const uint32_t base = static_cast<uint32_t>(cgl) * static_cast<uint32_t>(a.in_gstride) + col_off(qx, geo);
 #pragma unroll
         for (int h = 0; h < 2; ++h)
-            cbase[h] = gx < a.groups ? base + static_cast<uint32_t>((w.lane >> 4) + 4 * h) * geo.sub : OOR;
+            cbase[h] = ok ? base + static_cast<uint32_t>((w.lane >> 4) + 4 * h) * geo.sub : OOR;
     }
 
     template <int Y0, int NR>
@@ -311,22 +295,43 @@ struct Sink {
         scr = scratch;
         const int t = w.lane & 15;
         const long long colx = w.col0 + (w.c - w.lane) + 4 * t;  // first column of chunk t
-        const int gx = static_cast<int>(colx / geo.nq);
+        const int gx = colx >= 0 ? static_cast<int>(colx / geo.nq) : -1;
         const int qx = static_cast<int>(colx - static_cast<long long>(gx) * geo.nq);
         const uint32_t base = static_cast<uint32_t>(gx - w.g_first) * static_cast<uint32_t>(a.out_gstride) +
                               col_off(qx, geo);
-        const bool ok = gx < a.groups;
+        const bool ok = colx >= w.lo && colx < w.hi;
+#ifdef SH_GEN_STORE_ALIGNED  // measurement build only (see store_row_dw)
+        const uint32_t sstride = 176, abase = (static_cast<uint32_t>(gx - w.g_first) * static_cast<uint32_t>(a.out_gstride) + 4u * qx) & ~15u;
+#else
+        const uint32_t sstride = static_cast<uint32_t>(geo.sub), abase = base;
+#endif
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int b = (w.lane >> 4) + 4 * h;
-            voff[h] = ok ? base + static_cast<uint32_t>(b) * geo.sub : OOR;
+            voff[h] = ok ? abase + static_cast<uint32_t>(b) * sstride : OOR;
+        }
+        sub = static_cast<uint32_t>(geo.sub);
+        {
+            const long long colc = w.col0 + w.c;
+            const int gc = colc >= 0 ? static_cast<int>(colc / geo.nq) : -1;
+            const int qc = static_cast<int>(colc - static_cast<long long>(gc) * geo.nq);
+            dw_off = (colc >= w.lo && colc < w.hi)
+                         ? static_cast<uint32_t>(gc - w.g_first) * static_cast<uint32_t>(a.out_gstride) + col_off(qc, geo)
+                         : OOR;
         }
     }
+    // Measurement-only store forms (tools/gen_fixed_kernels.py SH_GEN_STORE): 1 = one dword
+    // store per sub-block straight from the registers; 2 = the transposed dwordx4 form at
+    // 16-byte-aligned offsets (sub-block stride rounded up to 176: wrong bytes, alignment cost).
+    uint32_t dw_off;          // this lane's column offset (dword form)
+    __device__ __forceinline__ void store_row_dw(int y, const uint32_t (&w)[8]) const {
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+            __builtin_amdgcn_raw_buffer_store_b32(w[b], rsrc, dw_off + static_cast<uint32_t>(b) * sub,
+                                                  static_cast<uint32_t>(y) * B, SH_STORE_AUX);
+    }
+    uint32_t sub;
     __device__ __forceinline__ void store_row(int y, const uint32_t (&w)[8]) const {
-#ifdef SH_EXPERIMENT_NO_STORE  // timing experiment only: keep the values, drop the stores
-        asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]), "v"(w[6]), "v"(w[7]));
-        return;
-#endif
 #pragma unroll
         for (int b = 0; b < 8; ++b) reinterpret_cast<uint32_t *>(scr)[b * 64 + lane] = w[b];
 #pragma unroll
@@ -338,52 +343,42 @@ struct Sink {
     }
 };
 
-// XCD-aware tile order. Workgroups are dealt round-robin over the 8 XCDs (block b -> XCD b % 8;
-// a speed assumption, never a correctness one). Adjacent column tiles usually split a group, so
-// both read the same 128-byte lines at their shared edge; giving them blocks b and b + 8 puts
-// them on one XCD at about the same time, and the second read hits that XCD's L2 instead of
-// going to HBM again (measured: 29% over-fetch on the staging microbenchmark without it).
-// Bijective map of block b in [0, n) to a tile: XCD i gets the contiguous tile range
-// [start_i, start_i + count_i), count_i = n/8 (+1 for the first n%8 XCDs).
-__device__ __forceinline__ int xcd_tile(int b, int n) {
-    const int q = n >> 3, r = n & 7;
-    const int x = b & 7, i = b >> 3;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
-}
-
-// Sets up src/sink, issues the ring's first R-1 DMAs and returns this wave's part. The caller
-// (the FIXED_KERNEL macro) then calls the generated run_<name> directly, so everything inlines
-// into one function: a non-inlined body took `src` by reference through scratch and read the
-// LDS ring with flat loads.
+// Sets up src/sink for the tile starting at column col0 (columns outside [lo, hi) are idle
+// lanes), issues the ring's first R-1 DMAs and returns this wave's part. The caller (the FIXED_KERNEL macro)
+// then calls the generated run_<name> directly, so everything inlines into one function: a
+// non-inlined body took `src` by reference through scratch and read the LDS ring with flat loads.
 template <class S, bool DEC>
 __device__ __forceinline__ int kernel_prologue(const FixedArgs &a, uint8_t *lds, Src<S, DEC> &src,
-                                               Sink &sink) {
+                                               Sink &sink, long long col0, long long lo, long long hi) {
     WGInfo w;
     w.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     w.lane = threadIdx.x & 63;
     const int part = w.wave % S::P;
     const int cw = w.wave / S::P;
     w.c = cw * 64 + w.lane;
-    w.col0 = static_cast<long long>(xcd_tile(blockIdx.x, gridDim.x)) * S::COLS;
+    w.col0 = col0;
+    w.lo = lo;
+    w.hi = hi;
     const int nq = a.geo.nq;
-    w.g_first = static_cast<int>(w.col0 / nq);
+    w.g_first = static_cast<int>((col0 > lo ? col0 : lo) / nq);
     const long long col = w.col0 + w.c;
-    const int g = static_cast<int>(col / nq);
+    w.valid = col >= lo && col < hi;
+    const int g = w.valid ? static_cast<int>(col / nq) : w.g_first;
     w.q = static_cast<int>(col - static_cast<long long>(g) * nq);
     w.gl = g - w.g_first;
-    w.valid = g < a.groups;
     // The store scratch (2 KB per wave) aliases the start of the ring: it is used only after the
     // last step, behind Src::release()'s barrier, so the ring gets that LDS as extra slots.
     static_assert(S::R * S::SLOT >= S::NW * 2048, "scratch must fit inside the ring");
     uint8_t *lds_pos = lds + S::R * S::SLOT;
     if (DEC) {
         const int ng = a.groups_per_wg;
+        const int ghi = static_cast<int>(hi / nq);
         constexpr int TW = (S::KP + S::MP) / 4;
         for (int i = threadIdx.x; i < ng * TW; i += S::NT) {
             const int lg = i / TW, t = i - lg * TW;
             const int gg = w.g_first + lg;
             uint32_t v = 0xFFFFFFFFu;
-            if (gg < a.groups) {
+            if (gg < ghi) {
                 v = (t < S::KP / 4)
                         ? reinterpret_cast<const uint32_t *>(a.pos + gg * static_cast<long long>(S::KP))[t]
                         : reinterpret_cast<const uint32_t *>(a.rpos + gg * static_cast<long long>(S::MP))[t - S::KP / 4];
@@ -395,18 +390,36 @@ __device__ __forceinline__ int kernel_prologue(const FixedArgs &a, uint8_t *lds,
     src.init(a, w, lds, lds_pos);
     if (DEC) src.init_items(a, w, lds + w.wave * 2048);
     sink.init(a, w, lds + w.wave * 2048);
+    if (S::DMA) {
 #pragma unroll
-    for (int x = 0; x < S::R - 1 && x < S::K; ++x) src.issue(x, src.pre(x));
+        for (int x = 0; x < S::R - 1 && x < S::K; ++x) src.issue(x, src.pre(x));
+    }
     return part;
 }
 
-template <class S>
-inline hipError_t launch_shape(FixedArgs a, bool dec, hipStream_t s, void (*kern)(FixedArgs)) {
+// XCD-aware tile order. Workgroups are dealt round-robin over the 8 XCDs (block b -> XCD b % 8;
+// a speed assumption, never a correctness one). Adjacent column tiles usually split a group, so
+// both read the same 128-byte lines at their shared edge; giving them blocks b and b + 8 puts
+// them on one XCD at about the same time, and the second read hits that XCD's L2 instead of
+// going to HBM again (measured: 29% over-fetch on the staging microbenchmark without it; a
+// persistent variant that walked each workgroup's own group range tile by tile re-read those
+// lines from memory: +30% FETCH_SIZE, 0.94 vs 0.75 ms, round 2). Bijective map of block b in
+// [0, n) to a tile: XCD i gets the contiguous tile range [start_i, start_i + count_i),
+// count_i = n/8 (+1 for the first n%8 XCDs).
+__device__ __forceinline__ int xcd_tile(int b, int n) {
+    const int q = n >> 3, r = n & 7;
+    const int x = b & 7, i = b >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
+template <class S, bool DEC>
+inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArgs)) {
+    constexpr bool dec = DEC;
     a.groups_per_wg = (S::COLS - 1) / a.geo.nq + 2;
-    const long long cols = static_cast<long long>(a.groups) * a.geo.nq;
-    const unsigned blocks = static_cast<unsigned>((cols + S::COLS - 1) / S::COLS);
     const size_t lds = static_cast<size_t>(S::R) * S::SLOT +  // ring (store scratch aliases it)
                        (dec ? static_cast<size_t>(a.groups_per_wg) * (S::KP + S::MP) : 0);
+    const long long cols = static_cast<long long>(a.groups) * a.geo.nq;
+    const unsigned blocks = static_cast<unsigned>((cols + S::COLS - 1) / S::COLS);  // one tile each
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(S::NT), lds, s, a);
     return hipGetLastError();
 }
@@ -414,35 +427,24 @@ inline hipError_t launch_shape(FixedArgs a, bool dec, hipStream_t s, void (*kern
 }  // namespace fixed
 }  // namespace sh
 
-#ifdef SH_EXPERIMENT_STAMPS
-#define SH_STAMPS_OUT(a, src)                                                                      \
-    if ((threadIdx.x & 63) == 0 && a.dbg) {                                                       \
-        unsigned long long t;                                                                     \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");               \
-        unsigned long long *d = a.dbg + (static_cast<size_t>(blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6)) * 4; \
-        d[0] = src.st_vm; d[1] = src.st_bar; d[2] = src.st_t0; d[3] = t;                          \
-    }
-#else
-#define SH_STAMPS_OUT(a, src)
-#endif
-
 // One kernel + launcher of a generated (k, m): MODE enc (DEC = false) or dec (DEC = true);
 // MINW = waves per SIMD the registers are allocated for. The host routes shapes with
 // nq % 4 != 0 (a 16-byte chunk could straddle two groups) or sub < 16 to the generic kernel.
-#define FIXED_KERNEL(NAME, K, M, P, CW, R, MINW, MODE, DEC)                                       \
+#define FIXED_KERNEL(NAME, K, M, P, CW, R, MINW, MODE, DEC, DMA)                                  \
     namespace sh {                                                                                \
     namespace fixed {                                                                             \
     __global__ __launch_bounds__(64 * CW * P, MINW) void kern_##NAME##_##MODE(FixedArgs a) {      \
         extern __shared__ __attribute__((aligned(16))) uint8_t lds[];                             \
-        using S = Shape<K, M, P, CW, R>;                                                          \
+        using S = Shape<K, M, P, CW, R, DMA>;                                                     \
         Src<S, DEC> src;                                                                          \
         Sink sink;                                                                                \
-        const int part = kernel_prologue<S, DEC>(a, lds, src, sink);                              \
+        const long long c0 = static_cast<long long>(xcd_tile(blockIdx.x, gridDim.x)) * S::COLS;  \
+        const int part = kernel_prologue<S, DEC>(a, lds, src, sink, c0, 0,                       \
+                                                 static_cast<long long>(a.groups) * a.geo.nq);   \
         run_##NAME(part, src, sink);                                                              \
-        SH_STAMPS_OUT(a, src);                                                                    \
     }                                                                                             \
     hipError_t launch_##NAME##_##MODE(FixedArgs a, hipStream_t s) {                               \
-        return launch_shape<Shape<K, M, P, CW, R>>(a, DEC, s, kern_##NAME##_##MODE);              \
+        return launch_shape<Shape<K, M, P, CW, R, DMA>, DEC>(a, s, kern_##NAME##_##MODE);         \
     }                                                                                             \
     }                                                                                             \
     }

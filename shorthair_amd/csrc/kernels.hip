@@ -243,7 +243,7 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
     __shared__ uint8_t s_exp[512];
     __shared__ uint8_t s_log[256];
     __shared__ uint8_t s_rows[256];
-    __shared__ uint8_t s_present[256];
+    __shared__ int s_present[256];      // occurrences of each row value
     __shared__ uint8_t s_rec[256];      // array index of the i-th recovery block
     __shared__ uint8_t s_rrow[256];     // its generator row r_i = row - k
     __shared__ uint8_t s_era[256];      // j-th erased original row E_j
@@ -261,8 +261,19 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
     for (int j = lane; j < k; j += 64) s_rows[j] = rows[j];
     __syncthreads();
     for (int j = lane; j < k; j += 64)
-        if (s_rows[j] < k) s_present[s_rows[j]] = 1;
+        atomicAdd(&s_present[s_rows[j]], 1);
     __syncthreads();
+    // A row listed twice, or a recovery row past the generator (row >= k + m), is outside the
+    // reference's contract (it would decode garbage): the group is left untouched and reported.
+    bool bad = false;
+    for (int r = lane; r < 256; r += 64) bad |= s_present[r] > 1 || (r >= k + m && s_present[r] > 0);
+    if (__ballot(bad) != 0ull) {
+        if (lane == 0) {
+            a.e_out[g] = -1;
+            if (a.errors) atomicAdd(a.errors, 1);
+        }
+        return;
+    }
 
     // Ordered compaction with wave ballots (the workgroup is one wave).
     int nrec = 0;
@@ -306,7 +317,10 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
     }
     if (e == 0) return;
     if (nera < e) {  // more recovery blocks than erasures: outside the reference's contract
-        if (lane == 0) a.e_out[g] = -1;
+        if (lane == 0) {
+            a.e_out[g] = -1;
+            if (a.errors) atomicAdd(a.errors, 1);
+        }
         return;
     }
     const int emax = a.emax;
@@ -336,14 +350,27 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
         }
     }
 
-    // Stage-B coefficients, transposed for the snippet kernel: coefB[col][j] = S^-1[j][i] with
-    // col = r_i (fixed path: rows of the residual) or i (generic path); zero elsewhere.
-    uint8_t *Bc = a.coefB + static_cast<long long>(g) * a.coefB_gstride;
-    const int ncol = fixed_mode ? m : emax;
-    for (int t = lane; t < ncol * a.ldB; t += 64) Bc[t] = 0;
+    // Stage-B coefficients, transposed ([i][j] = S^-1[j][i]). Generic path: bytes for the
+    // copy-and-XOR snippet kernel, zero elsewhere. Fixed path: the address of the accumulating
+    // snippet of each coefficient (the null snippet for zeros and for outputs j >= e), plus the
+    // residual row of each received recovery block.
+    uint8_t *Bc = fixed_mode ? nullptr : a.coefB + static_cast<long long>(g) * a.coefB_gstride;
+    // fixed layout [g][j / 8][i][j % 8]: one wave's 8 addresses of consecutive rows are contiguous
+    uint64_t *Tg = fixed_mode ? a.targets + static_cast<long long>(g) * emax * a.ldB : nullptr;
+    const uint64_t tnull = a.snip_base + static_cast<uint64_t>(SNIP_NULL) * SNIP_STRIDE;
+    if (fixed_mode) {
+        uint8_t *rr = a.rrow + static_cast<long long>(g) * emax;
+        for (int i = lane; i < e; i += 64) rr[i] = s_rrow[i];
+        for (int t = lane; t < emax * a.ldB; t += 64) Tg[t] = tnull;
+    } else {
+        for (int t = lane; t < emax * a.ldB; t += 64) Bc[t] = 0;
+    }
     auto put = [&](int j, int i, uint32_t v) {
-        const int col = fixed_mode ? s_rrow[i] : i;
-        Bc[static_cast<long long>(col) * a.ldB + j] = static_cast<uint8_t>(v);
+        if (fixed_mode)
+            Tg[(static_cast<long long>(j >> 3) * emax + i) * 8 + (j & 7)] =
+                v ? a.snip_base + static_cast<uint64_t>(v) * SNIP_STRIDE : tnull;
+        else
+            Bc[static_cast<long long>(i) * a.ldB + j] = static_cast<uint8_t>(v);
     };
     if (m >= 7) {
         for (int t = lane; t < e; t += 64) {
@@ -395,7 +422,10 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
         __syncthreads();
         const int p = s_piv;
         if (p < 0) {  // singular: impossible for an MDS submatrix
-            if (lane == 0) a.e_out[g] = -1;
+            if (lane == 0) {
+                a.e_out[g] = -1;
+                if (a.errors) atomicAdd(a.errors, 1);
+            }
             return;
         }
         if (lane < w && p != col) {

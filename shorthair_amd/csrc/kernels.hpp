@@ -59,14 +59,18 @@ struct DecodeSetupArgs {
     uint8_t *coefA;         // [G][emax][ldA]
     long long coefA_gstride;
     int ldA;
-    uint8_t *coefB;         // stage-B coefficients, TRANSPOSED: [G][n_in][ldB], entry [y][j]
+    uint8_t *coefB;         // generic mode: stage-B coefficients, TRANSPOSED [G][emax][ldB], entry [i][j]
     long long coefB_gstride;
     int ldB;                // >= emax, multiple of 8
     // Fixed-kernel mode (coefA == nullptr): stage A runs the compile-time generator over all m
-    // rows, so the setup emits position tables instead of stage-A coefficients, and stage B's
-    // coefficients are indexed by generator row y (coefB[l][y], ldB >= m) rather than by i.
+    // rows, so the setup emits position tables instead of stage-A coefficients, and stage B gets
+    // the residual row of each received recovery block plus ready-made snippet addresses.
     uint8_t *pos;           // [G][round4(k)] array index of original row x (0xFF = erased)
     uint8_t *rpos;          // [G][round4(m)] array index of recovery row y (0xFF = absent)
+    uint8_t *rrow;          // [G][emax] generator row r_i of the i-th received recovery block
+    uint64_t *targets;      // [G][ldB/8][emax][8]: address of the stage-B snippet of S^-1[j][i] at [j/8][i][j%8]
+    uint64_t snip_base;     // address of snippet 0 (stage-B snippet table, stride SNIP_STRIDE)
+    int *errors;            // device counter: groups with more recovery blocks than erasures
 };
 
 struct ScatterArgs {
@@ -83,11 +87,10 @@ struct ScatterArgs {
     int B;
 };
 
-// Decode stage B (csrc/stageb.hip): out[g][j] = sum_y M(coefT[g][y][j]) in[g][y], j < e[g].
+// Decode stage B, generic path (csrc/stageb.hip): out[g][j] = sum_i M(coefT[g][i][j]) in[g][i], j < e[g].
 struct StageBArgs {
     const uint8_t *in;        // [G][n_in][B] residual rows (>= 4 readable slack bytes at the end)
     long long in_gstride;
-    long long in_slack;       // readable bytes past groups * in_gstride
     int n_in;
     uint8_t *out;             // [G][emax][B]
     long long out_gstride;
@@ -97,9 +100,30 @@ struct StageBArgs {
     int ldT;
     int groups;
     Geometry geo;
-    unsigned long long *dbg;  // diagnostic builds only (SH_EXPERIMENT_STAMPS): per-wave phase stamps
 };
 hipError_t launch_stageb(const StageBArgs &a, int emax, hipStream_t stream);
+
+// Decode stage B, compile-time path: out[g][j] = sum_{i < e} M(S^-1[j][i]) in[g][rrow[g][i]]
+// with the coefficients given as snippet addresses (DecodeSetupArgs::targets).
+struct StageBFixedArgs {
+    const uint8_t *in;        // [G][n_in][B] residual rows (all m generator rows)
+    long long in_gstride;
+    uint8_t *out;             // [G][emax][B]
+    long long out_gstride;
+    const int *e;             // [G] received recovery blocks = outputs (<= 0: nothing to do)
+    const uint8_t *rrow;      // [G][emax]
+    const uint64_t *targets;  // [G][ldT/8][emax][8], entry [j/8][i][j%8]
+    int emax;
+    int ldT;                  // multiple of 8
+    int groups;
+    Geometry geo;
+};
+bool stageb_fixed_ok(const Geometry &geo, int emax);
+hipError_t launch_stageb_fixed(const StageBFixedArgs &a, hipStream_t stream);
+// Address of stage-B snippet 0 in the loaded code object (one tiny kernel launch + copy).
+hipError_t stageb_snip_base(uint64_t *out_host, hipStream_t stream);
+constexpr int SNIP_STRIDE = 72;   // bytes per stage-B snippet (gen_fixed_kernels.py)
+constexpr int SNIP_NULL = 256;    // index of the null snippet
 
 // Compile-time-scheduled kernels (csrc/gen/, tools/gen_fixed_kernels.py).
 struct FixedArgs {
@@ -114,7 +138,6 @@ struct FixedArgs {
     const uint8_t *pos;       // decode: [G][round4(k)] array index of original row x, 0xFF = erased
     const uint8_t *rpos;      // decode: [G][round4(m)] array index of recovery row y, 0xFF = absent
     int groups_per_wg;        // set by the launcher
-    unsigned long long *dbg;  // diagnostic builds only (SH_EXPERIMENT_STAMPS): per-wave cycle stamps
 };
 
 // Returns hipErrorNotSupported (and launches nothing) when (k, m) has no generated kernel or the

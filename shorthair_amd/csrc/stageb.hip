@@ -1,20 +1,20 @@
-// Runtime-coefficient bitmatrix product through a table of compile-time snippets (decode stage B).
+// Decode stage B: runtime-coefficient bitmatrix products through tables of compile-time snippets.
 //
-//   out[g][j] = sum_y M(coef[g][y][j]) * in[g][y]        (j < e_g outputs, y < n_in inputs)
+//   out[g][j] = sum_i M(coef[g][i][j]) * in[g][i]        (j < e_g outputs, i < e_g inputs)
 //
 // The coefficients (S^-1 of a group's erasure pattern) are only known at run time, so the
 // compile-time schedule of the encode kernels does not apply, and a register table indexed by a
 // runtime (wave-uniform) value costs 8.7x (hipcc's s_set_gpr_idx lowering). Here the
 // runtime choice is made ONCE per coefficient instead of once per table lookup: 256 snippets,
-// one per coefficient value c, each computing tmp[b] = T0[lo(c*2^b)] ^ T1[hi(c*2^b)] for b = 0..7
-// with compile-time register operands, are emitted inside the kernel (csrc/gen/snippets.h); the
-// kernel reaches snippet c with one s_swappc_b64 and returns with s_setpc_b64. The window tables
-// T0/T1 of the current input (the reference's win_encode tables, cauchy_256.cpp:1426-1445) and
-// tmp live in VGPRs pinned through explicit-register asm operands, so hipcc keeps its own values
-// out of them.
+// one per coefficient value c, each applying M(c) to the current input row from its window
+// tables (the reference's win_encode tables, cauchy_256.cpp:1426-1445) held in pinned VGPRs,
+// are emitted as code (csrc/gen/snippets.h); the kernel reaches snippet c with one s_swappc_b64
+// and the snippet returns with s_setpc_b64.
 //
-// One workgroup = one group x 64 word columns x 32 outputs (4 waves x 8 outputs). Group-uniform
-// coefficients require a wave to stay inside one group: at B = 1400 a group has 44 word columns.
+// Two kernels: stageb_snip (generic path, any geometry; copy-and-XOR snippets, coefficients as
+// bytes) and stageb_fixed (after a compile-time stage A: accumulating snippets in VGPR-index
+// mode, setup-computed snippet addresses, LDS-staged residual tile). Group-uniform coefficients
+// require a wave to stay inside one group: at B = 1400 a group has 44 word columns.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -22,7 +22,6 @@
 #include "snippets.h"
 
 #include <algorithm>
-#include <cstdlib>
 
 namespace sh {
 
@@ -42,8 +41,6 @@ __device__ __forceinline__ uint32_t ldw_b(const uint8_t *p) {
                  : [tg] "s"(target), "{v[100:115]}"(t0), "{v[116:131]}"(t1)                      \
                  : "s40", "s41")
 
-static_assert(SH_SNIPA_ACC == 32 && SH_SNIPA_T0 == 96 && SH_SNIPA_T1 == 112,
-              "accumulating-snippet registers must match the asm constraints");
 static_assert(SH_SNIP_T0 == 100 && SH_SNIP_T1 == 116 && SH_SNIP_TMP == 132,
               "snippet registers must match the call constraints");
 
@@ -130,314 +127,199 @@ __global__ __launch_bounds__(256) void stageb_snip(StageBArgs a) {
     }
 }
 
-// LDS-staged variant (the fixed-generator decode path: n_in <= 32, nq % 4 == 0, sub >= 16). One
-// workgroup = one group x one 64-column chunk x 32 outputs (4 waves x 8). The group's residual
-// rows for the chunk (n_in x 8 sub-blocks x ncols words, <= 64 KB) are gathered into LDS by
-// LDS-DMA up front, so the loop over input rows reads LDS (the next row prefetched into
-// registers under the current row's snippet calls) instead of waiting on HBM once per row.
-// Columns follow the fixed kernels' layout: the last 4-column chunk of each sub-block is
-// shifted back to end at the sub-block's end (fixed_common.hpp), so loads and stores are whole
-// dwords with no tail handling.
+// ---------------------------------------------------------------------------------------------
+// Compile-time path (after a generated stage-A kernel, csrc/gen/): one workgroup = one group x
+// one 64-column chunk x 32 outputs (4 waves x 8 outputs j0..j0+7).
+//
+//   out[j] = sum_{i < e} M(S^-1[j][i]) residual[rrow[i]]      (reference :1233-1392 semantics)
+//
+// The decode setup hands over, per group, the residual row r_i of each received recovery block
+// (compacted: only the e rows that exist are staged and visited, so the work scales with e^2)
+// and, for every (i, j), the ABSOLUTE address of the snippet that applies M(S^-1[j][i])
+// (snippet 256 = return at once for zero / unused entries). The row loop therefore does no
+// scalar address arithmetic: per input row it reads the 8 sub-block words from LDS, builds the
+// two 4-bit window tables (reference win_encode tables, cauchy_256.cpp:1426-1445, 22 XORs) into
+// the pinned registers v[96:127], and makes 8 calls into the snippet table in VGPR-index mode
+// (accumulator set j at v[32+8j..]). The residual tile is gathered into LDS by LDS-DMA with a
+// compile-time slot width W >= columns, so every LDS read has an immediate offset.
+// ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t colx_off(int q, int nq, int sub) {
     return 4u * q - (q >= nq - 4 ? static_cast<uint32_t>(4 * nq - sub) : 0u);
 }
 
 typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(3))) uint8_t lds_u8_t;
 
-__global__ __launch_bounds__(256, 3) void stageb_lds(StageBArgs a) {
-    SH_SNIPPET_TABLE(L);
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const Geometry geo = a.geo;
-    const int ncc = (geo.nq + 63) / 64;
-    const int g = blockIdx.x / ncc;
-    const int cc = blockIdx.x - g * ncc;
-    const int c0 = cc * 64;
-    const int ncols = min(64, geo.nq - c0);
-    const int nch = ncols / 4;        // 16-byte chunks per (row, sub-block)
-    const int cpb = nch * 16;         // LDS bytes per (row, sub-block)
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int e = a.e[g];
-    const int j0 = (blockIdx.y * 4 + wave) * 8;
-
-    // ---- gather the residual tile into LDS: chunk ch = (y*8 + a)*nch + t; then the group's
-    // stage-B coefficients (n_in x ldT bytes) behind it
-    const int total = a.n_in * 8 * nch;
-    const int tile = ((total + 255) / 256) * 256 * 16;
-    uint8_t *lcoef = lds + tile;
-    {
-        const long long gbase = static_cast<long long>(g) * a.in_gstride;
-        long long avail = static_cast<long long>(a.groups) * a.in_gstride + a.in_slack - gbase;
-        if (avail > 0x7FFFFFFFll) avail = 0x7FFFFFFFll;
-        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint8_t *>(a.in + gbase), static_cast<short>(0), static_cast<int>(avail), 0x00020000);
-        for (int base = wave * 64; base < total; base += 256) {  // uniform
-            const int ch = base + lane;
-            uint32_t off = 0x80000000u;
-            if (ch < total) {
-                const int ya = ch / nch, t = ch - ya * nch;
-                const int y = ya >> 3, sa = ya & 7;
-                off = static_cast<uint32_t>(y) * geo.B + static_cast<uint32_t>(sa) * geo.sub +
-                      colx_off(c0 + 4 * t, geo.nq, geo.sub);
-            }
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t *)(lds + base * 16), 16, off, 0, 0, 0);
-        }
-        const int cbytes = a.n_in * a.ldT;  // multiple of 8; <= 32 * 32
-        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint8_t *>(a.coefT + static_cast<long long>(g) * a.coefT_gstride), static_cast<short>(0),
-            cbytes, 0x00020000);
-        for (int base = wave * 64; base * 16 < cbytes; base += 256)  // uniform
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rc, (lds_void_t *)(lcoef + base * 16), 16, (base + lane) * 16, 0, 0, 0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
-    if (j0 >= e) return;  // wave-uniform (after the barrier)
-
-    uint64_t snip;
+// Holds the stage-B snippet table; its only launch reports where the table was loaded.
+__global__ void stageb_snip_probe(uint64_t *out) {
+    SH_SNIPA_TABLE(P);
+    uint64_t base;
     asm volatile(
         "s_getpc_b64 s[42:43]\n"
-        "s_add_u32 s42, s42, sh_snip_baseL@rel32@lo+4\n"
-        "s_addc_u32 s43, s43, sh_snip_baseL@rel32@hi+12\n"
+        "s_add_u32 s42, s42, sh_snipa_baseP@rel32@lo+4\n"
+        "s_addc_u32 s43, s43, sh_snipa_baseP@rel32@hi+12\n"
         "s_mov_b64 %0, s[42:43]"
-        : "=s"(snip)
+        : "=s"(base)
         :
         : "s42", "s43", "scc");
-
-    const uint8_t *rd = lds + 4 * lane;
-    const uint8_t *cf = lcoef + j0;
-
-    uint32_t acc[8][8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-        for (int b = 0; b < 8; ++b) acc[j][b] = 0;
-
-    // rows and coefficients are prefetched one input row ahead (LDS latency under the calls)
-    uint32_t d[8], dn[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s) d[s] = *reinterpret_cast<const uint32_t *>(rd + s * cpb);
-    uint2 cv = *reinterpret_cast<const uint2 *>(cf);
-    for (int y = 0; y < a.n_in; ++y) {
-        const int yn = y + 1 < a.n_in ? y + 1 : y;
-#pragma unroll
-        for (int s = 0; s < 8; ++s) dn[s] = *reinterpret_cast<const uint32_t *>(rd + (yn * 8 + s) * cpb);
-        const uint2 cvn = *reinterpret_cast<const uint2 *>(cf + yn * a.ldT);
-        const uint32_t clo = __builtin_amdgcn_readfirstlane(cv.x), chi = __builtin_amdgcn_readfirstlane(cv.y);
-        if ((clo | chi) != 0) {  // wave-uniform: no output of this wave uses input y otherwise
-            u32x16 t0, t1;
-            t0[0] = 0;
-            t1[0] = 0;
-            t0[1] = d[0]; t0[2] = d[1]; t0[4] = d[2]; t0[8] = d[3];
-            t1[1] = d[4]; t1[2] = d[5]; t1[4] = d[6]; t1[8] = d[7];
-            t0[3] = t0[1] ^ t0[2]; t0[5] = t0[1] ^ t0[4]; t0[6] = t0[2] ^ t0[4]; t0[7] = t0[3] ^ t0[4];
-            t0[9] = t0[1] ^ t0[8]; t0[10] = t0[2] ^ t0[8]; t0[11] = t0[3] ^ t0[8]; t0[12] = t0[4] ^ t0[8];
-            t0[13] = t0[5] ^ t0[8]; t0[14] = t0[6] ^ t0[8]; t0[15] = t0[7] ^ t0[8];
-            t1[3] = t1[1] ^ t1[2]; t1[5] = t1[1] ^ t1[4]; t1[6] = t1[2] ^ t1[4]; t1[7] = t1[3] ^ t1[4];
-            t1[9] = t1[1] ^ t1[8]; t1[10] = t1[2] ^ t1[8]; t1[11] = t1[3] ^ t1[8]; t1[12] = t1[4] ^ t1[8];
-            t1[13] = t1[5] ^ t1[8]; t1[14] = t1[6] ^ t1[8]; t1[15] = t1[7] ^ t1[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                // dense S^-1 (every coefficient of a received row is nonzero for e = m): no per-j
-                // skip; a zero coefficient simply runs snippet 0 (adds nothing)
-                const uint32_t c = ((j < 4 ? clo : chi) >> (8 * (j & 3))) & 0xffu;
-                u32x8 tmp;
-#ifndef SH_EXPERIMENT_NO_CALL
-                SH_SNIP_CALL(snip + (static_cast<uint64_t>(c) << 6), t0, t1, tmp);
-#else  // timing experiment only: the table work and accumulation without the call
-                for (int b = 0; b < 8; ++b) tmp[b] = t0[(c + b) & 15] ^ t1[(c >> 4 + b) & 15];
-#endif
-#ifndef SH_EXPERIMENT_NO_ACC
-#pragma unroll
-                for (int b = 0; b < 8; ++b) acc[j][b] ^= tmp[b];
-#else
-                if (j == 0)
-                    for (int b = 0; b < 8; ++b) acc[0][b] ^= tmp[b];
-#endif
-            }
-        }
-#pragma unroll
-        for (int s = 0; s < 8; ++s) d[s] = dn[s];
-        cv = cvn;
-    }
-
-    if (lane >= ncols) return;
-    const uint32_t col = colx_off(c0 + lane, geo.nq, geo.sub);
-    uint8_t *out = a.out + static_cast<long long>(g) * a.out_gstride + col;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        if (j0 + j >= e) break;
-        uint8_t *row = out + static_cast<long long>(j0 + j) * geo.B;
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const uint32_t w = acc[j][b];
-            __builtin_memcpy(row + b * geo.sub, &w, 4);
-        }
-    }
+    if (threadIdx.x == 0) *out = base;
 }
 
-#ifdef SH_EXPERIMENT_INLINE_SNIP  // timing experiment: fixed inline snippet, no branches
-#define SH_CALLX(G) "v_bitop3_b32 v64, v64, v129, v146 bitop3:0x96\n""v_bitop3_b32 v65, v65, v132, v151 bitop3:0x96\n""v_bitop3_b32 v66, v66, v135, v156 bitop3:0x96\n""v_bitop3_b32 v67, v67, v138, v145 bitop3:0x96\n""v_bitop3_b32 v68, v68, v141, v150 bitop3:0x96\n""v_bitop3_b32 v69, v69, v128, v155 bitop3:0x96\n""v_bitop3_b32 v70, v70, v131, v144 bitop3:0x96\n""v_bitop3_b32 v71, v71, v134, v149 bitop3:0x96\n"
-#else
-#define SH_CALLX(G) "s_swappc_b64 s[40:41], %[" #G "]\n"
-#endif
-#ifdef SH_EXPERIMENT_NO_ROWS  // timing experiment: wrong results, no per-row compute
-#define SH_ROWS_ON false
-#else
-#define SH_ROWS_ON true
-#endif
-#ifdef SH_EXPERIMENT_NO_GPRIDX  // timing experiment: wrong results, no VGPR-index mode
-#define SH_GI_ON ""
-#define SH_GI_IDX(n) ""
-#define SH_GI_OFF ""
-#else
-#define SH_GI_ON "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"
-#define SH_GI_IDX(n) "s_set_gpr_idx_idx " n "\n"
-#define SH_GI_OFF "s_set_gpr_idx_off"
-#endif
-#ifdef SH_EXPERIMENT_STAMPS
-#define SH_BSTAMP(i)                                                                               \
-    do {                                                                                           \
-        unsigned long long t_;                                                                     \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
-        st_[i] = t_;                                                                               \
-    } while (0)
-#else
-#define SH_BSTAMP(i)
-#endif
+static_assert(SH_SNIPA_ACC == 32 && SH_SNIPA_T0 == 96 && SH_SNIPA_T1 == 112,
+              "accumulating-snippet registers must match the asm constraints");
+static_assert(SH_SNIPA_STRIDE == SNIP_STRIDE && SH_SNIPA_NULL == SNIP_NULL, "snippet table layout");
 
-__global__ __launch_bounds__(256, 3) void stageb_acc(StageBArgs a) {
-    SH_SNIPA_TABLE(A);
+// One input row: 8 LDS words -> window tables -> 8 snippet calls. O1..O7: byte offsets of
+// sub-blocks 1..7 in the LDS tile (a * W * 4).
+#define SH_ROW_ASM(O1, O2, O3, O4, O5, O6, O7)                                                   \
+    "ds_read_b32 v97, %[ad]\n"                                                                    \
+    "ds_read_b32 v98, %[ad] offset:" #O1 "\n"                                                     \
+    "ds_read_b32 v100, %[ad] offset:" #O2 "\n"                                                    \
+    "ds_read_b32 v104, %[ad] offset:" #O3 "\n"                                                    \
+    "ds_read_b32 v113, %[ad] offset:" #O4 "\n"                                                    \
+    "ds_read_b32 v114, %[ad] offset:" #O5 "\n"                                                    \
+    "ds_read_b32 v116, %[ad] offset:" #O6 "\n"                                                    \
+    "ds_read_b32 v120, %[ad] offset:" #O7 "\n"                                                    \
+    "s_waitcnt lgkmcnt(0)\n"                                                                      \
+    "v_xor_b32 v99, v97, v98\n"                                                                   \
+    "v_xor_b32 v115, v113, v114\n"                                                                \
+    "v_xor_b32 v101, v97, v100\n"                                                                 \
+    "v_xor_b32 v117, v113, v116\n"                                                                \
+    "v_xor_b32 v102, v98, v100\n"                                                                 \
+    "v_xor_b32 v118, v114, v116\n"                                                                \
+    "v_xor_b32 v105, v97, v104\n"                                                                 \
+    "v_xor_b32 v121, v113, v120\n"                                                                \
+    "v_xor_b32 v106, v98, v104\n"                                                                 \
+    "v_xor_b32 v122, v114, v120\n"                                                                \
+    "v_xor_b32 v108, v100, v104\n"                                                                \
+    "v_xor_b32 v124, v116, v120\n"                                                                \
+    "v_xor_b32 v103, v99, v100\n"                                                                 \
+    "v_xor_b32 v119, v115, v116\n"                                                                \
+    "v_xor_b32 v107, v99, v104\n"                                                                 \
+    "v_xor_b32 v123, v115, v120\n"                                                                \
+    "v_xor_b32 v109, v101, v104\n"                                                                \
+    "v_xor_b32 v125, v117, v120\n"                                                                \
+    "v_xor_b32 v110, v102, v104\n"                                                                \
+    "v_xor_b32 v126, v118, v120\n"                                                                \
+    "v_xor_b32 v111, v103, v104\n"                                                                \
+    "v_xor_b32 v127, v119, v120\n"                                                                \
+    "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"                                                     \
+    "s_swappc_b64 s[40:41], %[g0]\n"                                                              \
+    "s_set_gpr_idx_idx 8\n"                                                                       \
+    "s_swappc_b64 s[40:41], %[g1]\n"                                                              \
+    "s_set_gpr_idx_idx 16\n"                                                                      \
+    "s_swappc_b64 s[40:41], %[g2]\n"                                                              \
+    "s_set_gpr_idx_idx 24\n"                                                                      \
+    "s_swappc_b64 s[40:41], %[g3]\n"                                                              \
+    "s_set_gpr_idx_idx 32\n"                                                                      \
+    "s_swappc_b64 s[40:41], %[g4]\n"                                                              \
+    "s_set_gpr_idx_idx 40\n"                                                                      \
+    "s_swappc_b64 s[40:41], %[g5]\n"                                                              \
+    "s_set_gpr_idx_idx 48\n"                                                                      \
+    "s_swappc_b64 s[40:41], %[g6]\n"                                                              \
+    "s_set_gpr_idx_idx 56\n"                                                                      \
+    "s_swappc_b64 s[40:41], %[g7]\n"                                                              \
+    "s_set_gpr_idx_off"
+
+template <int W> struct RowAsm;
+#define SH_ROW_W(WW, O1, O2, O3, O4, O5, O6, O7)                                                  \
+    template <> struct RowAsm<WW> {                                                               \
+        static __device__ __forceinline__ void run(uint32_t ad, const uint64_t (&tg)[8], u32x16 &a01, \
+                                                   u32x16 &a23, u32x16 &a45, u32x16 &a67,         \
+                                                   uint32_t &z0, uint32_t &z1) {                  \
+            asm volatile(SH_ROW_ASM(O1, O2, O3, O4, O5, O6, O7)                                   \
+                         : "+{v[32:47]}"(a01), "+{v[48:63]}"(a23), "+{v[64:79]}"(a45),            \
+                           "+{v[80:95]}"(a67), "+{v96}"(z0), "+{v112}"(z1)                         \
+                         : [ad] "v"(ad), [g0] "s"(tg[0]), [g1] "s"(tg[1]), [g2] "s"(tg[2]),       \
+                           [g3] "s"(tg[3]), [g4] "s"(tg[4]), [g5] "s"(tg[5]), [g6] "s"(tg[6]),    \
+                           [g7] "s"(tg[7])                                                        \
+                         : "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105",   \
+                           "v106", "v107", "v108", "v109", "v110", "v111", "v113", "v114",        \
+                           "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122",        \
+                           "v123", "v124", "v125", "v126", "v127", "s40", "s41", "m0", "memory"); \
+        }                                                                                         \
+    };
+SH_ROW_W(16, 64, 128, 192, 256, 320, 384, 448)
+SH_ROW_W(32, 128, 256, 384, 512, 640, 768, 896)
+SH_ROW_W(48, 192, 384, 576, 768, 960, 1152, 1344)
+SH_ROW_W(64, 256, 512, 768, 1024, 1280, 1536, 1792)
+#undef SH_ROW_W
+
+template <int W>
+__global__ __launch_bounds__(256, 3) void stageb_fixed(StageBFixedArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr int CPS = W / 4;  // 16-byte chunk slots per (row, sub-block) in LDS
     const Geometry geo = a.geo;
     const int ncc = (geo.nq + 63) / 64;
     const int g = blockIdx.x / ncc;
     const int cc = blockIdx.x - g * ncc;
     const int c0 = cc * 64;
     const int ncols = min(64, geo.nq - c0);
-    const int nch = ncols / 4;        // 16-byte chunks per (row, sub-block)
-    const int cpb = nch * 16;         // LDS bytes per (row, sub-block)
+    const int nch = ncols >> 2;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-#ifdef SH_EXPERIMENT_STAMPS
-    unsigned long long st_[6];
-#endif
-    SH_BSTAMP(0);
     const int e = a.e[g];
-#ifdef SH_EXPERIMENT_STAMPS
-    asm volatile("" ::"s"(e));
-#endif
-    SH_BSTAMP(1);
-    const int j0 = (blockIdx.y * 4 + wave) * 8;
+    if (e <= 0) return;  // uniform over the workgroup: no barrier reached yet
 
-    // ---- gather the residual tile into LDS: chunk ch = (y*8 + a)*nch + t; then the group's
-    // stage-B coefficients (n_in x ldT bytes) behind it
-    const int total = a.n_in * 8 * nch;
-    const int tile = ((total + 255) / 256) * 256 * 16;
-    uint8_t *lcoef = lds + tile;
+    // ---- gather the e received residual rows of this chunk into LDS: slot (i, sub-block s) at
+    // ((i * 8 + s) * W) words; chunk t (4 columns) of a slot at +16 t; t >= nch pads with zeros
     {
+        const uint8_t *rr = a.rrow + static_cast<long long>(g) * a.emax;
         const long long gbase = static_cast<long long>(g) * a.in_gstride;
-        long long avail = static_cast<long long>(a.groups) * a.in_gstride + a.in_slack - gbase;
+        long long avail = static_cast<long long>(a.groups) * a.in_gstride - gbase;
         if (avail > 0x7FFFFFFFll) avail = 0x7FFFFFFFll;
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<uint8_t *>(a.in + gbase), static_cast<short>(0), static_cast<int>(avail), 0x00020000);
+        const int total = e * 8 * CPS;
         for (int base = wave * 64; base < total; base += 256) {  // uniform
             const int ch = base + lane;
             uint32_t off = 0x80000000u;
             if (ch < total) {
-                const int ya = ch / nch, t = ch - ya * nch;
-                const int y = ya >> 3, sa = ya & 7;
-                off = static_cast<uint32_t>(y) * geo.B + static_cast<uint32_t>(sa) * geo.sub +
-                      colx_off(c0 + 4 * t, geo.nq, geo.sub);
+                const int is = ch / CPS, t = ch - is * CPS;
+                if (t < nch)
+                    off = static_cast<uint32_t>(rr[is >> 3]) * geo.B + static_cast<uint32_t>(is & 7) * geo.sub +
+                          colx_off(c0 + 4 * t, geo.nq, geo.sub);
             }
             __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t *)(lds + base * 16), 16, off, 0, 0, 0);
         }
-        const int cbytes = a.n_in * a.ldT;  // multiple of 8; <= 32 * 32
-        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint8_t *>(a.coefT + static_cast<long long>(g) * a.coefT_gstride), static_cast<short>(0),
-            cbytes, 0x00020000);
-        for (int base = wave * 64; base * 16 < cbytes; base += 256)  // uniform
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rc, (lds_void_t *)(lcoef + base * 16), 16, (base + lane) * 16, 0, 0, 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-    if (j0 >= e) return;  // wave-uniform (after the barrier)
-    SH_BSTAMP(2);
+    const int j0 = (blockIdx.y * 4 + wave) * 8;
+    if (j0 >= e) return;  // wave-uniform, after the only barrier
 
-    uint64_t snip;
-    asm volatile(
-        "s_getpc_b64 s[42:43]\n"
-        "s_add_u32 s42, s42, sh_snipa_baseA@rel32@lo+4\n"
-        "s_addc_u32 s43, s43, sh_snipa_baseA@rel32@hi+12\n"
-        "s_mov_b64 %0, s[42:43]"
-        : "=s"(snip)
-        :
-        : "s42", "s43", "scc");
-
-    const uint8_t *rd = lds + 4 * lane;
-    const uint8_t *cf = lcoef + j0;
-
-    // accumulators pinned to v[32:95] (output j at v[32+8j..]), window tables to v[96:127]
     u32x16 a01, a23, a45, a67;
 #pragma unroll
     for (int i = 0; i < 16; ++i) a01[i] = a23[i] = a45[i] = a67[i] = 0;
-
-    // rows and coefficients are prefetched one input row ahead (LDS latency under the calls)
-    uint32_t d[8], dn[8];
+    uint32_t z0 = 0, z1 = 0;  // window-table entry 0 of each half (v96, v112)
+    // This wave's snippet addresses: [i][8] contiguous (setup layout [g][j/8][i][8]). Constant
+    // address space, so the uniform loads become s_load_dwordx16; four rows are loaded per wait
+    // (the row asm's lgkmcnt(0) also covers scalar loads, so each batch's latency shows once).
+    typedef const __attribute__((address_space(4))) uint64_t cu64_t;
+    const cu64_t *tp = (const cu64_t *)(a.targets + (static_cast<long long>(g) * (a.ldT / 8) + (j0 >> 3)) * a.emax * 8);
+    uint32_t ad = static_cast<uint32_t>(reinterpret_cast<size_t>((lds_u8_t *)lds)) + 4u * lane;
+    int i = 0;
+    for (; i + 4 <= e; i += 4) {
+        uint64_t tg[4][8];
 #pragma unroll
-    for (int s = 0; s < 8; ++s) d[s] = *reinterpret_cast<const uint32_t *>(rd + s * cpb);
-    uint2 cv = *reinterpret_cast<const uint2 *>(cf);
-    for (int y = 0; y < a.n_in; ++y) {
-        const int yn = y + 1 < a.n_in ? y + 1 : y;
+        for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int s = 0; s < 8; ++s) dn[s] = *reinterpret_cast<const uint32_t *>(rd + (yn * 8 + s) * cpb);
-        const uint2 cvn = *reinterpret_cast<const uint2 *>(cf + yn * a.ldT);
-        const uint32_t clo = __builtin_amdgcn_readfirstlane(cv.x), chi = __builtin_amdgcn_readfirstlane(cv.y);
-        if (SH_ROWS_ON && (clo | chi) != 0) {  // wave-uniform: no output of this wave uses input y otherwise
-            u32x16 t0, t1;
-            t0[0] = 0;
-            t1[0] = 0;
-            t0[1] = d[0]; t0[2] = d[1]; t0[4] = d[2]; t0[8] = d[3];
-            t1[1] = d[4]; t1[2] = d[5]; t1[4] = d[6]; t1[8] = d[7];
-            t0[3] = t0[1] ^ t0[2]; t0[5] = t0[1] ^ t0[4]; t0[6] = t0[2] ^ t0[4]; t0[7] = t0[3] ^ t0[4];
-            t0[9] = t0[1] ^ t0[8]; t0[10] = t0[2] ^ t0[8]; t0[11] = t0[3] ^ t0[8]; t0[12] = t0[4] ^ t0[8];
-            t0[13] = t0[5] ^ t0[8]; t0[14] = t0[6] ^ t0[8]; t0[15] = t0[7] ^ t0[8];
-            t1[3] = t1[1] ^ t1[2]; t1[5] = t1[1] ^ t1[4]; t1[6] = t1[2] ^ t1[4]; t1[7] = t1[3] ^ t1[4];
-            t1[9] = t1[1] ^ t1[8]; t1[10] = t1[2] ^ t1[8]; t1[11] = t1[3] ^ t1[8]; t1[12] = t1[4] ^ t1[8];
-            t1[13] = t1[5] ^ t1[8]; t1[14] = t1[6] ^ t1[8]; t1[15] = t1[7] ^ t1[8];
-            uint64_t tg[8];
+            for (int j = 0; j < 8; ++j) tg[r][j] = tp[(i + r) * 8 + j];
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-                tg[j] = snip + (static_cast<uint64_t>(((j < 4 ? clo : chi) >> (8 * (j & 3))) & 0xffu) << 7);
-            // One asm block: VGPR-index mode must not see any compiler VALU between on and off.
-            asm volatile(
-                SH_GI_ON
-                SH_CALLX(g0)
-                SH_GI_IDX("8")
-                SH_CALLX(g1)
-                SH_GI_IDX("16")
-                SH_CALLX(g2)
-                SH_GI_IDX("24")
-                SH_CALLX(g3)
-                SH_GI_IDX("32")
-                SH_CALLX(g4)
-                SH_GI_IDX("40")
-                SH_CALLX(g5)
-                SH_GI_IDX("48")
-                SH_CALLX(g6)
-                SH_GI_IDX("56")
-                SH_CALLX(g7)
-                SH_GI_OFF
-                : "+{v[32:47]}"(a01), "+{v[48:63]}"(a23), "+{v[64:79]}"(a45), "+{v[80:95]}"(a67)
-                : "{v[96:111]}"(t0), "{v[112:127]}"(t1), [g0] "s"(tg[0]), [g1] "s"(tg[1]),
-                  [g2] "s"(tg[2]), [g3] "s"(tg[3]), [g4] "s"(tg[4]), [g5] "s"(tg[5]), [g6] "s"(tg[6]),
-                  [g7] "s"(tg[7])
-                : "s40", "s41", "m0", "memory");
+        for (int r = 0; r < 4; ++r) {
+            RowAsm<W>::run(ad, tg[r], a01, a23, a45, a67, z0, z1);
+            ad += 8 * W * 4;
         }
-#pragma unroll
-        for (int s = 0; s < 8; ++s) d[s] = dn[s];
-        cv = cvn;
     }
-    SH_BSTAMP(3);
+    for (; i < e; ++i) {
+        uint64_t tg[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) tg[j] = tp[i * 8 + j];
+        RowAsm<W>::run(ad, tg, a01, a23, a45, a67, z0, z1);
+        ad += 8 * W * 4;
+    }
+
+    if (lane >= ncols) return;
     uint32_t acc[8][8];
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
@@ -446,8 +328,6 @@ __global__ __launch_bounds__(256, 3) void stageb_acc(StageBArgs a) {
         acc[4][b] = a45[b]; acc[5][b] = a45[8 + b];
         acc[6][b] = a67[b]; acc[7][b] = a67[8 + b];
     }
-
-    if (lane < ncols) {
     const uint32_t col = colx_off(c0 + lane, geo.nq, geo.sub);
     uint8_t *out = a.out + static_cast<long long>(g) * a.out_gstride + col;
 #pragma unroll
@@ -455,42 +335,211 @@ __global__ __launch_bounds__(256, 3) void stageb_acc(StageBArgs a) {
         if (j0 + j >= e) break;
         uint8_t *row = out + static_cast<long long>(j0 + j) * geo.B;
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const uint32_t w = acc[j][b];
-            __builtin_memcpy(row + b * geo.sub, &w, 4);
-        }
-    }    }
-#ifdef SH_EXPERIMENT_STAMPS
-    SH_BSTAMP(4);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    SH_BSTAMP(5);
-    if (lane == 0 && a.dbg) {
-        unsigned long long *d = a.dbg + ((static_cast<size_t>(blockIdx.y) * gridDim.x + blockIdx.x) * 4 + wave) * 8;
-        for (int t = 0; t < 6; ++t) d[t] = st_[t];
+        for (int b = 0; b < 8; ++b) __builtin_memcpy(row + b * geo.sub, &acc[j][b], 4);
     }
-#endif
+}
+// Streaming variant: no LDS tile. Each wave loads its own residual rows with buffer loads,
+// prefetched two rows ahead into registers and waited for with its own vmcnt (no barrier), so
+// there is no serialized tile prologue and occupancy is set by registers (4 waves per SIMD).
+// The 4 waves of a group read the same rows (L2 hits after the first).
+#define SH_ROW_ASM_R                                                                              \
+    "v_mov_b32 v97, %[d0]\n"                                                                      \
+    "v_mov_b32 v98, %[d1]\n"                                                                      \
+    "v_mov_b32 v100, %[d2]\n"                                                                     \
+    "v_mov_b32 v104, %[d3]\n"                                                                     \
+    "v_mov_b32 v113, %[d4]\n"                                                                     \
+    "v_mov_b32 v114, %[d5]\n"                                                                     \
+    "v_mov_b32 v116, %[d6]\n"                                                                     \
+    "v_mov_b32 v120, %[d7]\n"                                                                     \
+    "v_xor_b32 v99, %[d0], %[d1]\n"                                                               \
+    "v_xor_b32 v115, %[d4], %[d5]\n"                                                              \
+    "v_xor_b32 v101, %[d0], %[d2]\n"                                                              \
+    "v_xor_b32 v117, %[d4], %[d6]\n"                                                              \
+    "v_xor_b32 v102, %[d1], %[d2]\n"                                                              \
+    "v_xor_b32 v118, %[d5], %[d6]\n"                                                              \
+    "v_xor_b32 v105, %[d0], %[d3]\n"                                                              \
+    "v_xor_b32 v121, %[d4], %[d7]\n"                                                              \
+    "v_xor_b32 v106, %[d1], %[d3]\n"                                                              \
+    "v_xor_b32 v122, %[d5], %[d7]\n"                                                              \
+    "v_xor_b32 v108, %[d2], %[d3]\n"                                                              \
+    "v_xor_b32 v124, %[d6], %[d7]\n"                                                              \
+    "v_xor_b32 v103, v99, %[d2]\n"                                                                \
+    "v_xor_b32 v119, v115, %[d6]\n"                                                               \
+    "v_xor_b32 v107, v99, %[d3]\n"                                                                \
+    "v_xor_b32 v123, v115, %[d7]\n"                                                               \
+    "v_xor_b32 v109, v101, %[d3]\n"                                                               \
+    "v_xor_b32 v125, v117, %[d7]\n"                                                               \
+    "v_xor_b32 v110, v102, %[d3]\n"                                                               \
+    "v_xor_b32 v126, v118, %[d7]\n"                                                               \
+    "v_xor_b32 v111, v103, %[d3]\n"                                                               \
+    "v_xor_b32 v127, v119, %[d7]\n"                                                               \
+    "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"                                                     \
+    "s_swappc_b64 s[40:41], %[g0]\n"                                                              \
+    "s_set_gpr_idx_idx 8\n"                                                                       \
+    "s_swappc_b64 s[40:41], %[g1]\n"                                                              \
+    "s_set_gpr_idx_idx 16\n"                                                                      \
+    "s_swappc_b64 s[40:41], %[g2]\n"                                                              \
+    "s_set_gpr_idx_idx 24\n"                                                                      \
+    "s_swappc_b64 s[40:41], %[g3]\n"                                                              \
+    "s_set_gpr_idx_idx 32\n"                                                                      \
+    "s_swappc_b64 s[40:41], %[g4]\n"                                                              \
+    "s_set_gpr_idx_idx 40\n"                                                                      \
+    "s_swappc_b64 s[40:41], %[g5]\n"                                                              \
+    "s_set_gpr_idx_idx 48\n"                                                                      \
+    "s_swappc_b64 s[40:41], %[g6]\n"                                                              \
+    "s_set_gpr_idx_idx 56\n"                                                                      \
+    "s_swappc_b64 s[40:41], %[g7]\n"                                                              \
+    "s_set_gpr_idx_off"
+
+struct Row8 {
+    uint32_t w[8];
+};
+
+__device__ __forceinline__ void row_regs(const Row8 &d, const uint64_t (&tg)[8], u32x16 &a01, u32x16 &a23,
+                                         u32x16 &a45, u32x16 &a67, uint32_t &z0, uint32_t &z1) {
+    asm volatile(SH_ROW_ASM_R
+                 : "+{v[32:47]}"(a01), "+{v[48:63]}"(a23), "+{v[64:79]}"(a45), "+{v[80:95]}"(a67),
+                   "+{v96}"(z0), "+{v112}"(z1)
+                 : [d0] "v"(d.w[0]), [d1] "v"(d.w[1]), [d2] "v"(d.w[2]), [d3] "v"(d.w[3]), [d4] "v"(d.w[4]),
+                   [d5] "v"(d.w[5]), [d6] "v"(d.w[6]), [d7] "v"(d.w[7]), [g0] "s"(tg[0]), [g1] "s"(tg[1]),
+                   [g2] "s"(tg[2]), [g3] "s"(tg[3]), [g4] "s"(tg[4]), [g5] "s"(tg[5]), [g6] "s"(tg[6]),
+                   [g7] "s"(tg[7])
+                 : "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107",
+                   "v108", "v109", "v110", "v111", "v113", "v114", "v115", "v116", "v117", "v118", "v119",
+                   "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "s40", "s41", "m0", "memory");
 }
 
-bool stageb_lds_ok(const StageBArgs &a) {
-    return a.n_in <= 32 && a.ldT <= 32 && a.geo.nq % 4 == 0 && a.geo.sub >= 16;
+__global__ __launch_bounds__(256, 4) void stageb_stream(StageBFixedArgs a) {
+    const Geometry geo = a.geo;
+    const int ncc = (geo.nq + 63) / 64;
+    const int g = blockIdx.x / ncc;
+    const int cc = blockIdx.x - g * ncc;
+    const int c0 = cc * 64;
+    const int ncols = min(64, geo.nq - c0);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int e = a.e[g];
+    const int j0 = (blockIdx.y * 4 + wave) * 8;
+    if (j0 >= e) return;  // wave-uniform; e <= 0 included
+    // idle lanes (lane >= ncols) load a valid column of the group and store nothing
+    const uint32_t col = colx_off(c0 + min(lane, ncols - 1), geo.nq, geo.sub);
+    uint32_t voff[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) voff[s] = col + static_cast<uint32_t>(s) * geo.sub;
+    const long long gbase = static_cast<long long>(g) * a.in_gstride;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.in + gbase), static_cast<short>(0), static_cast<int>(a.in_gstride), 0x00020000);
+    // scalar loads (gfx950 has no sub-dword s_load: read the row list as dwords)
+    typedef const __attribute__((address_space(4))) uint32_t cu32_t;
+    typedef const __attribute__((address_space(4))) uint64_t cu64_t;
+    const cu32_t *rr = (const cu32_t *)(a.rrow + static_cast<long long>(g) * a.emax);  // emax % 4 == 0 rows
+    const cu64_t *tp = (const cu64_t *)(a.targets + (static_cast<long long>(g) * (a.ldT / 8) + (j0 >> 3)) * a.emax * 8);
+    auto load_row = [&](int i, Row8 &d) {
+        const uint32_t soff = ((rr[i >> 2] >> (8 * (i & 3))) & 0xFFu) * static_cast<uint32_t>(geo.B);
+#pragma unroll
+        for (int s = 0; s < 8; ++s) d.w[s] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff[s], soff, 0);
+    };
+
+    u32x16 a01, a23, a45, a67;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) a01[t] = a23[t] = a45[t] = a67[t] = 0;
+    uint32_t z0 = 0, z1 = 0;
+    Row8 r0, r1, r2;
+    load_row(0, r0);
+    if (e > 1) load_row(1, r1);
+    int i = 0;
+    for (; i + 3 <= e; i += 3) {  // rows i, i+1, i+2 in r0, r1, r2 (rotating, two rows in flight)
+        uint64_t tg[8];
+        if (i + 2 < e) load_row(i + 2, r2);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) tg[j] = tp[i * 8 + j];
+        row_regs(r0, tg, a01, a23, a45, a67, z0, z1);
+        if (i + 3 < e) load_row(i + 3, r0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) tg[j] = tp[(i + 1) * 8 + j];
+        row_regs(r1, tg, a01, a23, a45, a67, z0, z1);
+        if (i + 4 < e) load_row(i + 4, r1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) tg[j] = tp[(i + 2) * 8 + j];
+        row_regs(r2, tg, a01, a23, a45, a67, z0, z1);
+    }
+    if (i < e) {  // one or two rows left, in r0 (and r1)
+        uint64_t tg[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) tg[j] = tp[i * 8 + j];
+        row_regs(r0, tg, a01, a23, a45, a67, z0, z1);
+        if (i + 1 < e) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) tg[j] = tp[(i + 1) * 8 + j];
+            row_regs(r1, tg, a01, a23, a45, a67, z0, z1);
+        }
+    }
+
+    if (lane >= ncols) return;
+    uint32_t acc[8][8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        acc[0][b] = a01[b]; acc[1][b] = a01[8 + b];
+        acc[2][b] = a23[b]; acc[3][b] = a23[8 + b];
+        acc[4][b] = a45[b]; acc[5][b] = a45[8 + b];
+        acc[6][b] = a67[b]; acc[7][b] = a67[8 + b];
+    }
+    uint8_t *out = a.out + static_cast<long long>(g) * a.out_gstride + colx_off(c0 + lane, geo.nq, geo.sub);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (j0 + j >= e) break;
+        uint8_t *row = out + static_cast<long long>(j0 + j) * geo.B;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) __builtin_memcpy(row + b * geo.sub, &acc[j][b], 4);
+    }
+}
+
+static int stageb_w(int ncols) { return ncols <= 16 ? 16 : ncols <= 32 ? 32 : ncols <= 48 ? 48 : 64; }
+
+static size_t stageb_fixed_lds(const Geometry &geo, int emax) {
+    const int W = stageb_w(std::min(64, geo.nq));
+    const size_t chunks = static_cast<size_t>(emax) * 8 * (W / 4);
+    return ((chunks + 255) / 256) * 256 * 16;  // whole 4-wave DMA rounds (idle lanes write zeros)
+}
+
+bool stageb_fixed_ok(const Geometry &geo, int emax) {
+    // 16-byte chunks stay inside one sub-block (nq % 4 == 0, shifted last chunk: sub >= 16)
+    return geo.nq % 4 == 0 && geo.sub >= 16 && emax >= 1 && stageb_fixed_lds(geo, emax) <= 160 * 1024;
+}
+
+hipError_t launch_stageb_fixed(const StageBFixedArgs &a, hipStream_t stream) {
+    if (a.groups <= 0 || a.emax <= 0) return hipSuccess;
+    if (!stageb_fixed_ok(a.geo, a.emax)) return hipErrorNotSupported;
+    const int ncc = (a.geo.nq + 63) / 64;
+    const size_t lds = stageb_fixed_lds(a.geo, a.emax);
+    dim3 grid(static_cast<unsigned>(ncc) * a.groups, (a.emax + 31) / 32, 1);
+#ifdef SH_STAGEB_STREAM
+    hipLaunchKernelGGL(stageb_stream, grid, dim3(256), 0, stream, a);
+    return hipGetLastError();
+#endif
+    switch (stageb_w(std::min(64, a.geo.nq))) {
+        case 16: hipLaunchKernelGGL(stageb_fixed<16>, grid, dim3(256), lds, stream, a); break;
+        case 32: hipLaunchKernelGGL(stageb_fixed<32>, grid, dim3(256), lds, stream, a); break;
+        case 48: hipLaunchKernelGGL(stageb_fixed<48>, grid, dim3(256), lds, stream, a); break;
+        default: hipLaunchKernelGGL(stageb_fixed<64>, grid, dim3(256), lds, stream, a); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t stageb_snip_base(uint64_t *out_host, hipStream_t stream) {
+    uint64_t *d = nullptr;
+    hipError_t err = hipMalloc(&d, sizeof(uint64_t));
+    if (err != hipSuccess) return err;
+    hipLaunchKernelGGL(stageb_snip_probe, dim3(1), dim3(64), 0, stream, d);
+    err = hipGetLastError();
+    if (err == hipSuccess) err = hipMemcpyAsync(out_host, d, sizeof(uint64_t), hipMemcpyDeviceToHost, stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(stream);
+    (void)hipFree(d);
+    return err;
 }
 
 hipError_t launch_stageb(const StageBArgs &a, int emax, hipStream_t stream) {
     if (a.groups <= 0 || emax <= 0) return hipSuccess;
-    if (stageb_lds_ok(a)) {
-        const int ncc = (a.geo.nq + 63) / 64;
-        const int nch = std::min(64, a.geo.nq) / 4;
-        // tile bytes rounded up to whole 4-wave DMA rounds (out-of-range lanes still write LDS)
-        const size_t chunks = static_cast<size_t>(a.n_in) * 8 * nch;
-        const size_t cbytes = static_cast<size_t>(a.n_in) * a.ldT;  // coefficients behind the tile
-        const size_t lds = ((chunks + 255) / 256) * 256 * 16 + ((cbytes + 4095) / 4096) * 4096;
-        dim3 grid(static_cast<unsigned>(ncc) * a.groups, (emax + 31) / 32, 1);
-        if (std::getenv("SH_STAGEB_SNIP"))  // A/B switch: the copy-and-XOR snippet kernel
-            hipLaunchKernelGGL(stageb_lds, grid, dim3(256), lds, stream, a);
-        else
-            hipLaunchKernelGGL(stageb_acc, grid, dim3(256), lds, stream, a);
-        return hipGetLastError();
-    }
     dim3 grid(static_cast<unsigned>((a.geo.nq + 63) / 64) * a.groups, (emax + 31) / 32, 1);
     hipLaunchKernelGGL(stageb_snip, grid, dim3(256), 0, stream, a);
     return hipGetLastError();

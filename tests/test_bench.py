@@ -26,3 +26,35 @@ def test_traffic_lookup_requires_matching_build():
     assert bench.pmc_traffic(Fake, "dec", 200, 32, 1400, 8192, 32) == (None, None)
     t, src = bench.pmc_traffic(sh, "dec", 200, 32, 1400, 8192, 32)
     assert (t is None) == (src is None)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_launcher_spawns_ranks(n):
+    """`bench.py --gpus N` outside a launcher starts N rank processes (before any GPU call) with
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set; --dry-run joins them in a gloo group (no GPU)
+    and rank 0 reports what every rank saw."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1  # only rank 0 prints
+    d = json.loads(line[0])
+    assert d["dry_run"] and d["n_gpus"] == n and d["gpus_arg"] == n
+    ranks = d["ranks"]
+    assert [x["rank"] for x in ranks] == list(range(n))
+    assert all(x["local_rank"] == x["rank"] and x["world_size"] == n for x in ranks)
+    assert len({x["master_port"] for x in ranks}) == 1 and len({x["pid"] for x in ranks}) == n
+
+
+def test_cpu_baseline_native_modes():
+    import bench
+    if not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "cpu_bench")):
+        pytest.skip("oracle/_ref/cpu_bench not built")
+    cpu = bench.cpu_baseline(28, 4, 1400, 4, 0.2, 2)
+    assert set(cpu["modes"]) == {"shipped_t1", "init_t1", "shipped_t2", "init_t2"}
+    assert cpu["value"] == max(cpu["modes"]["shipped_t2"]["GiBps"], cpu["modes"]["init_t2"]["GiBps"])
+    assert cpu["cpu"]

@@ -264,3 +264,99 @@ def test_tiny_and_odd_block_sizes(sh):
         for g in range(G):
             _, exp = ora.encode(k, m, data[g], B)
             assert np.array_equal(d_out[g].cpu().numpy(), exp), (B, g)
+
+
+def test_decode_two_streams_concurrent(sh):
+    """Two batched decodes in flight at once on two streams, different erasure patterns: each
+    stream has its own decode workspace, so both results are exact."""
+    import torch
+    k, m, B, G = 200, 32, 1400, 768
+    runs = []
+    for cfg in (0x11, 0x22):
+        data, rec, blocks, d_rows, rows, es = _decode_inputs(k, m, B, G, cfg, 0)
+        out = torch.zeros((G, m, B), dtype=torch.uint8, device="cuda")
+        orow = torch.zeros((G, m), dtype=torch.uint8, device="cuda")
+        ocnt = torch.zeros(G, dtype=torch.int32, device="cuda")
+        runs.append((data, blocks, d_rows, es, out, orow, ocnt, torch.cuda.Stream()))
+    _sync()
+    for _ in range(3):
+        for data, blocks, d_rows, es, out, orow, ocnt, st in runs:
+            with torch.cuda.stream(st):
+                assert sh.decode_batch_out(k, m, B, G, blocks, d_rows, out, orow, ocnt,
+                                           stream=st.cuda_stream) == 0
+    _sync()
+    for data, blocks, d_rows, es, out, orow, ocnt, st in runs:
+        assert np.array_equal(ocnt.cpu().numpy(), es)
+        idx = orow.long()
+        truth = data[torch.arange(G, device="cuda")[:, None], idx]
+        mask = torch.arange(m, device="cuda")[None, :] < ocnt[:, None]
+        assert torch.equal(out[mask], truth[mask])
+
+
+def test_malformed_groups_reported(sh):
+    """A row listed twice (outside the reference's contract) leaves the group untouched, flags it
+    with count -1 and is counted by cauchy_256_batch_errors; the single-group call returns -1."""
+    import torch
+    k, m, B, G = 40, 8, 64, 4
+    assert sh.batch_errors() == 0
+    blocks = torch.randint(0, 256, (G, k, B), dtype=torch.uint8, device="cuda")
+    rows = torch.arange(k, dtype=torch.uint8, device="cuda").repeat(G, 1).contiguous()
+    rows[:, 0] = k       # every group: original 0 lost, recovery row 0 received (valid)
+    rows[2, 1] = k       # group 2: recovery row 0 listed twice (malformed)
+    before = blocks.clone()
+    out = torch.zeros((G, m, B), dtype=torch.uint8, device="cuda")
+    orow = torch.zeros((G, m), dtype=torch.uint8, device="cuda")
+    ocnt = torch.zeros(G, dtype=torch.int32, device="cuda")
+    assert sh.decode_batch_out(k, m, B, G, blocks, rows, out, orow, ocnt) == 0
+    assert sh.batch_errors() == 1
+    assert ocnt.cpu().numpy().tolist() == [1, 1, -1, 1]
+    r2 = rows.clone()
+    assert sh.decode_batch(k, m, B, G, blocks, r2) == 0
+    assert sh.batch_errors() == 1
+    assert torch.equal(blocks[2], before[2]) and torch.equal(r2[2], rows[2])
+    bufs = [np.zeros(B, np.uint8) for _ in range(k)]
+    arr = (sh.Block * k)()
+    rr = rows[2].cpu().numpy()
+    for i in range(k):
+        arr[i].data = bufs[i].ctypes.data
+        arr[i].row = int(rr[i])
+    assert sh.cauchy_256_decode(k, m, arr, B) == -1
+    assert sh.batch_errors() == 1
+
+
+def test_c5_per_gpu_shard_131072_groups(sh):
+    """BASELINE config C5 at its per-GPU shard size (1M groups over 8 GPUs = 131,072 groups of
+    k=200 m=32 B=1400 per GPU, 36.7 GB of input): one encode and one in-place decode launch over
+    the whole shard (every per-workgroup descriptor / 64-bit offset path at that size), the
+    encode -> erase -> decode round trip checked for EVERY group on the device, and sampled
+    groups (first, middle, last) against the oracle byte for byte."""
+    import torch
+    k, m, B, G, cfg = 200, 32, 1400, 131072, 0xC5
+    data = torch.empty((G, k, B), dtype=torch.uint8, device="cuda")
+    rec = torch.empty((G, m, B), dtype=torch.uint8, device="cuda")
+    assert sh.fill_synthetic(data, k, B, G, 0, cfg) == 0
+    assert sh.encode_batch(k, m, B, G, data, rec) == 0
+    rows = np.zeros((G, k), np.uint8)
+    for g in range(G):
+        rows[g] = sh.erasure_pattern(g, k, m, cfg, 0)[1]
+    d_rows = torch.from_numpy(rows).cuda()
+    gi = torch.arange(G, device="cuda")[:, None]
+    whole = torch.cat([data, rec], dim=1)
+    blocks = whole[gi, d_rows.long()]  # device memory peak ~ 4 x 37 GB of the 288 GB
+    del whole
+    sample = (0, G // 2, G - 1)
+    recv = {g: blocks[g].cpu().numpy() for g in sample}
+    assert sh.decode_batch(k, m, B, G, blocks, d_rows) == 0
+    _sync()
+    assert sh.batch_errors() == 0
+    new_rows = d_rows.long()
+    assert torch.equal(blocks, data[gi, new_rows]), "round trip"
+    ora = po.oracle()
+    for g in sample:
+        d = po.fill_group(g, k, B, cfg)
+        rc, exp = ora.encode(k, m, d, B)
+        assert rc == 0 and np.array_equal(rec[g].cpu().numpy(), exp), g
+        b = [x.copy() for x in recv[g]]
+        rc, nr = ora.decode(k, m, b, list(rows[g]), B)
+        assert rc == 0 and nr == d_rows[g].cpu().numpy().tolist(), g
+        assert np.array_equal(np.stack(b), blocks[g].cpu().numpy()), g

@@ -32,6 +32,11 @@ if os.environ.get("SH_CONFIGS"):  # experiments: e.g. SH_CONFIGS="200,32;64,16"
     CONFIGS = [tuple(map(int, c.split(","))) for c in os.environ["SH_CONFIGS"].split(";")]
 ROWS_PER_PART = int(os.environ.get("SH_ROWS_PER_PART", "8"))
 READ_PIN = os.environ.get("SH_READ_PIN", "0") == "1"
+# Measurement-only ablations for A/B libraries built by tools/build_variant.sh (never the product
+# default, results are wrong), comma-separated: "nodma" = no input DMA (compute on whatever the
+# ring holds), "novalu" = DMA, ring reads, barriers and stores but no XOR work, "nobar" = no
+# vmcnt wait / barrier (only meaningful with nodma), "nostore" = no output stores.
+ABLATE = set(filter(None, os.environ.get("SH_GEN_ABLATE", "").split(",")))
 
 
 def gf_tables():
@@ -148,9 +153,11 @@ class Body:
                 if (x + 1) % S == 0:
                     # group boundary: the next S blocks must have landed (counted vmcnt) and every
                     # wave must be past block x-1 (barrier), which frees the slots of blocks <= x-1
-                    L.append(f"    src.template wait<{min(k - 1, x + S)}, {nxt_issue}>();")
+                    if "nobar" not in ABLATE:
+                        L.append(f"    src.template wait<{min(k - 1, x + S)}, {nxt_issue}>();")
                     while nxt_issue < k and nxt_issue - R <= x - 1:
-                        L.append(f"    src.issue({nxt_issue}, pre);")
+                        if "nodma" not in ABLATE:
+                            L.append(f"    src.issue({nxt_issue}, pre);")
                         nxt_issue += 1
                         if nxt_issue < k:
                             L.append(f"    pre = src.pre({nxt_issue});")
@@ -170,13 +177,9 @@ class Body:
                     ups.append((v >> 4, v & 15, yi, b))
                     v = gmul(v, 2)
             ups.sort(key=lambda u: (u[0], u[1]))
-            if os.environ.get("SH_TABLES_FIRST"):  # experiment: build every needed entry first
-                for hi, lo, yi, b in ups:
-                    if lo:
-                        self.table_expr(0, lo, have, cur)
-                for hi, lo, yi, b in ups:
-                    if hi:
-                        self.table_expr(1, hi, have, cur)
+            if "novalu" in ABLATE:  # keep the loaded words alive, do no XOR work
+                L.append("    asm volatile(\"\" :: " + ", ".join(f'"v"({cur}{a})' for a in range(8)) + ");")
+                ups = []
             for hi, lo, yi, b in ups:
                 acc = f"acc[{yi}][{b}]"
                 if lo and hi:
@@ -255,15 +258,21 @@ def gen_config(k, m):
         out.append(f"    src.template epilogue<{y0}, {nr}>(acc);")
         for yi in range(nr):
             out.append("    __builtin_amdgcn_sched_barrier(0);")
-            out.append(f"    sink.store_row({y0 + yi}, acc[{yi}]);")
+            if "halfstore" in ABLATE and p >= len(parts) // 2:
+                out.append(f"    asm volatile(\"\" :: " + ", ".join(f'"v"(acc[{yi}][{b}])' for b in range(8)) + ");")
+            elif os.environ.get("SH_GEN_STORE") == "1":
+                out.append(f"    sink.store_row_dw({y0 + yi}, acc[{yi}]);")
+            elif "nostore" in ABLATE:
+                out.append(f"    asm volatile(\"\" :: " + ", ".join(f'"v"(acc[{yi}][{b}])' for b in range(8)) + ");")
+            else:
+                out.append(f"    sink.store_row({y0 + yi}, acc[{yi}]);")
         out.append("}")
         out.append("")
     out.append(f"template <class Src>")
     out.append(f"__device__ __forceinline__ void run_{name}(int part, const Src &src, const Sink &sink) {{")
-    same = os.environ.get("SH_EXPERIMENT_SAME_CODE")  # timing experiment only: wrong results
     for p in range(len(parts)):
         kw = "if" if p == 0 else "else if"
-        out.append(f"    {kw} (part == {p}) run_{name}_p{0 if same else p}(src, sink);")
+        out.append(f"    {kw} (part == {p}) run_{name}_p{p}(src, sink);")
     out.append("}")
     out.append("}  // namespace fixed")
     out.append("}  // namespace sh")
@@ -279,7 +288,8 @@ def gen_config(k, m):
         with open(path, "w") as f:
             f.write(f"// GENERATED by tools/gen_fixed_kernels.py -- do not edit. (k={k}, m={m}, {mode})\n"
                     f'#include "fixed_{name}.inc"\n'
-                    f"FIXED_KERNEL({name}, {k}, {m}, {P}, {CW}, {R}, {minw}, {mode}, {dec})\n")
+                    f"FIXED_KERNEL({name}, {k}, {m}, {P}, {CW}, {R}, {minw}, {mode}, {dec}, "
+                    f"{'false' if 'nodma' in ABLATE else 'true'})\n")
         paths.append(path)
     return paths
 
@@ -312,28 +322,32 @@ def gen_snippets():
             v = gmul(v, 2)
         lines.append('    "s_setpc_b64 s[40:41]\\n"')
     lines.append('    "sh_snip_end" #SFX ":\\n" ::: "memory")')
-    # Accumulating variant for VGPR-index mode (csrc/stageb.hip, stageb_acc): snippet c does
+    # Accumulating variant for VGPR-index mode (csrc/stageb.hip, stageb_fixed): snippet c does
     # acc[b] ^= T0[lo(c*2^b)] ^ T1[hi(c*2^b)] as 8 v_bitop3_b32 whose destination and first
     # source are relative to M0 (s_set_gpr_idx_on ..., gpr_idx(SRC0,DST)): the caller selects the
-    # output row with s_set_gpr_idx_idx, no copy-and-XOR of a temporary. 128-byte stride.
+    # output row with s_set_gpr_idx_idx, no copy-and-XOR of a temporary. Every snippet is exactly
+    # SNIPA_STRIDE = 72 bytes (8 x 8-byte bitop3 + s_setpc + s_nop), so snippet c sits at
+    # base + 72*c; entry 256 is the null snippet (zero coefficient / unused output: return at once).
+    # The decode setup writes absolute snippet addresses, so the stage-B loop computes no targets.
     acc = ['#define SH_SNIPA_ACC %d' % SNIPA_ACC, '#define SH_SNIPA_T0 %d' % SNIPA_T0,
-           '#define SH_SNIPA_T1 %d' % SNIPA_T1,
+           '#define SH_SNIPA_T1 %d' % SNIPA_T1, '#define SH_SNIPA_STRIDE 72', '#define SH_SNIPA_NULL 256',
            '#define SH_SNIPA_TABLE(SFX) asm volatile("s_branch sh_snipa_end" #SFX "\\n"',
-           '    ".p2align 7\\n"',
+           '    ".p2align 6\\n"',
            '    "sh_snipa_base" #SFX ":\\n"']
     for c in range(256):
         v = c
-        acc.append('    ".p2align 7\\n"')
         for b in range(8):
             lo, hi = v & 15, v >> 4
             acc.append(f'    "v_bitop3_b32 v{SNIPA_ACC + b}, v{SNIPA_ACC + b}, v{SNIPA_T0 + lo}, v{SNIPA_T1 + hi} bitop3:0x96\\n"')
             v = gmul(v, 2)
         acc.append('    "s_setpc_b64 s[40:41]\\n"')
+        acc.append('    "s_nop 0\\n"')
+    acc.append('    "s_setpc_b64 s[40:41]\\n"')
     acc.append('    "sh_snipa_end" #SFX ":\\n" ::: "memory")')
     with open(os.path.join(OUTDIR, "snippets.h"), "w") as f:
         f.write(lines[0] + "\n" + lines[1] + "\n" + lines[2] + "\n" + "\n".join(lines[3:6]) + "\n"
                 + " \\\n".join(lines[6:]) + "\n")
-        f.write("\n".join(acc[:3]) + "\n" + " \\\n".join(acc[3:]) + "\n")
+        f.write("\n".join(acc[:5]) + "\n" + " \\\n".join(acc[5:]) + "\n")
 
 
 def main(argv=()):

@@ -21,6 +21,7 @@ def main():
     p.add_argument("--block", type=int, default=1400)
     p.add_argument("--groups", type=int, default=8192)
     p.add_argument("--erasures", type=int, default=32)
+    p.add_argument("--concurrent", action="store_true", help="encode and decode on two streams at once")
     a = p.parse_args()
     import torch
     import shorthair_amd as sh
@@ -44,6 +45,32 @@ def main():
         ocnt = torch.empty(G, dtype=torch.int32, device="cuda")
         sh.batch_reserve(k, m, B, G)
     torch.cuda.synchronize()
+    if a.concurrent:
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for it in range(a.iters + 1):
+            if it == 1:
+                torch.cuda.synchronize()
+                e0.record()
+            ev_s = torch.cuda.Event()
+            ev_s.record()
+            s1.wait_event(ev_s)
+            s2.wait_event(ev_s)
+            sh.encode_batch(k, m, B, G, data, rec, s1.cuda_stream)
+            sh.decode_batch_out(k, m, B, G, blocks, d_rows, out, orow, ocnt, s2.cuda_stream)
+            d1, d2 = torch.cuda.Event(), torch.cuda.Event()
+            d1.record(s1)
+            d2.record(s2)
+            torch.cuda.current_stream().wait_event(d1)
+            torch.cuda.current_stream().wait_event(d2)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / a.iters
+        tot = G * (k + m) * B + G * (k + a.erasures) * B
+        print(f"{os.path.basename(sh.LIB_PATH)} concurrent encode||decode: {ms:.3f} ms per step "
+              f"({tot / ms / 1e6:.0f} GB/s, {tot / ms / 1e-3 / 2**30:.0f} GiB/s)")
+        return
+    sh.profile(a.iters)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     te = td = 0.0
     for _ in range(a.iters):
@@ -60,7 +87,8 @@ def main():
     enc_b = G * (k + m) * B
     dec_b = G * (k + a.erasures) * B
     print(f"{os.path.basename(sh.LIB_PATH)} {a.op}: encode {te / a.iters:.3f} ms ({enc_b / (te / a.iters) / 1e9:.0f} GB/s)"
-          f"  decode {td / a.iters:.3f} ms ({dec_b / (td / a.iters) / 1e9:.0f} GB/s)")
+          f"  decode {td / a.iters:.3f} ms ({dec_b / (td / a.iters) / 1e9:.0f} GB/s)"
+          + ("" if a.op == "encode" else "  stages setup/A/B ms: %s" % " / ".join(f"{x:.3f}" for x in (sh.profile_read() or ()))))
 
 
 if __name__ == "__main__":
