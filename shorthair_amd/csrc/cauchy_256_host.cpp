@@ -200,7 +200,7 @@ hipError_t launch_fixed_batch(int k, int m, int B, int groups, const uint8_t *in
     a.out_gstride = out_gs;
     a.out_bytes = static_cast<long long>(groups) * out_gs;
     a.groups = groups;
-    a.geo = sh::make_geometry(B);
+    a.geo = sh::fixed_geometry(B);
     a.pos = pos;
     a.rpos = rpos;
     return sh::launch_fixed(k, m, a, dec, s);
@@ -262,7 +262,7 @@ struct DecodeWS {
 };
 
 size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool need_recovered) {
-    const sh::Geometry geo = sh::make_geometry(B);
+    const sh::Geometry geo = sh::fixed_geometry(B);
     w.emax = std::min(k, m);
     w.fixed = sh::has_fixed(k, m, B) && sh::stageb_fixed_ok(geo, w.emax);
     w.ldA = w.fixed ? 0 : round4(k);
@@ -283,7 +283,7 @@ size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool n
     w.coefA = w.fixed ? nullptr : take(G * w.coefA_gs);
     w.coefB = w.fixed ? nullptr : take(G * w.coefB_gs);
     w.targets = w.fixed ? reinterpret_cast<uint64_t *>(take(G * w.emax * w.ldB * sizeof(uint64_t))) : nullptr;
-    w.rrow = w.fixed ? take(G * w.emax) : nullptr;
+    w.rrow = w.fixed ? take(G * round4(w.emax)) : nullptr;
     w.pos = w.fixed ? take(G * round4(k)) : nullptr;
     w.rpos = w.fixed ? take(G * round4(m)) : nullptr;
     w.residual = take(G * w.nres * static_cast<size_t>(B) + 256);  // + slack: word over-read
@@ -302,9 +302,10 @@ hipError_t launch_stage_b(const DecodeWS &w, int n_in, int B, int groups, uint8_
         f.rrow = w.rrow;
         f.targets = w.targets;
         f.emax = w.emax;
+        f.ldR = round4(w.emax);
         f.ldT = w.ldB;
         f.groups = groups;
-        f.geo = sh::make_geometry(B);
+        f.geo = sh::fixed_geometry(B);
         return sh::launch_stageb_fixed(f, s);
     }
     sh::StageBArgs b{};
@@ -351,6 +352,7 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
     sa.pos = w.pos;
     sa.rpos = w.rpos;
     sa.rrow = w.rrow;
+    sa.ldR = round4(w.emax);
     sa.targets = w.targets;
     sa.snip_base = c.snip_base;
     sa.errors = c.d_errors;

@@ -159,12 +159,17 @@ struct Src {
     }
 
     // Wait until this wave's DMAs of steps <= T are done (I = steps issued so far), then join the
-    // workgroup barrier. One asm statement: nothing is scheduled between the two.
+    // workgroup barrier. One asm statement: nothing is scheduled between the two. Waves that
+    // issue no DMA (NDMA < NW) only join the barrier: their vmcnt holds nothing but the previous
+    // tile's output stores, which nothing here needs to wait for.
     template <int T, int I>
-    __device__ __forceinline__ static void wait() {
+    __device__ __forceinline__ void wait() const {
         constexpr int N = (I - T - 1) * S::DPW;
         static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+        if (S::NDMA % S::NW != 0 && wave * S::DPW >= S::NDMA)
+            asm volatile("s_barrier" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
     }
 
     // After the last step: every wave's reads of the ring are done before any wave writes its

@@ -14,9 +14,8 @@ SH_FIXED_CONFIGS(SH_DECL)
 }  // namespace fixed
 
 bool has_fixed(int k, int m, int B) {
-    // 16-byte DMA chunks must not straddle two groups (nq = ceil(B/8 / 4) % 4 == 0) and the
-    // shifted last chunk must stay inside its sub-block (B/8 >= 16); see fixed_common.hpp.
-    if (B % 8 != 0 || B / 8 < 16 || ((B / 8 + 3) / 4) % 4 != 0) return false;
+    // the shifted last 16-byte chunk must stay inside its sub-block (B/8 >= 16; fixed_geometry)
+    if (B % 8 != 0 || B / 8 < 16) return false;
 #define SH_HAS(K, M) if (k == K && m == M) return true;
     SH_FIXED_CONFIGS(SH_HAS)
 #undef SH_HAS

@@ -359,7 +359,7 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
     uint64_t *Tg = fixed_mode ? a.targets + static_cast<long long>(g) * emax * a.ldB : nullptr;
     const uint64_t tnull = a.snip_base + static_cast<uint64_t>(SNIP_NULL) * SNIP_STRIDE;
     if (fixed_mode) {
-        uint8_t *rr = a.rrow + static_cast<long long>(g) * emax;
+        uint8_t *rr = a.rrow + static_cast<long long>(g) * a.ldR;
         for (int i = lane; i < e; i += 64) rr[i] = s_rrow[i];
         for (int t = lane; t < emax * a.ldB; t += 64) Tg[t] = tnull;
     } else {

@@ -25,6 +25,17 @@ inline Geometry make_geometry(int B) {
     return g;
 }
 
+// Geometry of the compile-time path: the word columns per sub-block are rounded up to a multiple
+// of 4 so 16-byte (4-column) chunks never straddle two groups; the last chunk of a sub-block is
+// shifted back by 4 * nq - sub (< 16) bytes so it ends at the sub-block's end (its first bytes
+// are computed twice, identically). Needs sub >= 16.
+inline Geometry fixed_geometry(int B) {
+    Geometry g = make_geometry(B);
+    g.nq = (g.nq + 3) & ~3;
+    g.tail = 4;
+    return g;
+}
+
 struct ApplyArgs {
     const uint8_t *in;
     long long in_gstride;   // bytes between groups
@@ -67,7 +78,8 @@ struct DecodeSetupArgs {
     // the residual row of each received recovery block plus ready-made snippet addresses.
     uint8_t *pos;           // [G][round4(k)] array index of original row x (0xFF = erased)
     uint8_t *rpos;          // [G][round4(m)] array index of recovery row y (0xFF = absent)
-    uint8_t *rrow;          // [G][emax] generator row r_i of the i-th received recovery block
+    uint8_t *rrow;          // [G][ldR] generator row r_i of the i-th received recovery block
+    int ldR;                // round4(emax)
     uint64_t *targets;      // [G][ldB/8][emax][8]: address of the stage-B snippet of S^-1[j][i] at [j/8][i][j%8]
     uint64_t snip_base;     // address of snippet 0 (stage-B snippet table, stride SNIP_STRIDE)
     int *errors;            // device counter: groups with more recovery blocks than erasures
@@ -111,9 +123,10 @@ struct StageBFixedArgs {
     uint8_t *out;             // [G][emax][B]
     long long out_gstride;
     const int *e;             // [G] received recovery blocks = outputs (<= 0: nothing to do)
-    const uint8_t *rrow;      // [G][emax]
+    const uint8_t *rrow;      // [G][ldR]
     const uint64_t *targets;  // [G][ldT/8][emax][8], entry [j/8][i][j%8]
     int emax;
+    int ldR;                  // round4(emax): row lists are read as dwords
     int ldT;                  // multiple of 8
     int groups;
     Geometry geo;
