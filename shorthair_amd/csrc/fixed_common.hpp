@@ -61,9 +61,12 @@ namespace fixed {
 // are instruction-fetch heavy); a non-volatile asm is opaque to reassociation yet schedulable.
 #define XV(acc, t) asm("v_xor_b32 %0, %1, %2" : "=v"(acc) : "v"(t), "v"(acc))
 
-// Cache policy of the output stores (aux operand of the buffer store).
+// Cache policy of the output stores and of the input DMA (aux operand of the buffer op).
 #ifndef SH_STORE_AUX
 #define SH_STORE_AUX 0
+#endif
+#ifndef SH_LOAD_AUX
+#define SH_LOAD_AUX 0
 #endif
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -178,19 +181,21 @@ struct Src {
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
 
-    // Decode: the DMA source of step x depends on the group's position table (LDS). pre(x) reads
-    // it one iteration before issue(x, .) needs it, so the DMA issue never waits on LDS latency.
+    // Decode: the DMA source of a step depends on the group's position table (LDS): entry t < KP
+    // is the array index of original column t, entry KP + y that of recovery row y (0xFF =
+    // absent). pre(t) reads it one iteration before issue(x, .) needs it, so the DMA issue never
+    // waits on LDS latency.
     struct Pre {
         int p[S::DPW];
     };
-    __device__ __forceinline__ Pre pre(int x) const {
+    __device__ __forceinline__ Pre pre(int t) const {
         Pre r;
 #pragma unroll
-        for (int j = 0; j < S::DPW; ++j) r.p[j] = DEC ? pos[dgl[j] * (S::KP + S::MP) + x] : 0;
+        for (int j = 0; j < S::DPW; ++j) r.p[j] = DEC ? pos[dgl[j] * (S::KP + S::MP) + t] : 0;
         return r;
     }
 
-    // DMA of input step x into its ring slot.
+    // DMA of step x into its ring slot (encode: input block x).
     __device__ __forceinline__ void issue(int x, const Pre &pr) const {
         uint8_t *slot = const_cast<uint8_t *>(lds) + (x % S::R) * S::SLOT;
 #pragma unroll
@@ -200,10 +205,10 @@ struct Src {
             if (DEC) {
                 const int p = pr.p[j];
                 const uint32_t o = (p == 0xFF || dbase[j] == OOR) ? OOR : dbase[j] + static_cast<uint32_t>(p) * B;
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, S::W, o, 0, 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, S::W, o, 0, 0, SH_LOAD_AUX);
             } else {
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, S::W, dbase[j],
-                                                         static_cast<uint32_t>(x) * B, 0, 0);
+                                                         static_cast<uint32_t>(x) * B, 0, SH_LOAD_AUX);
             }
         }
     }
@@ -222,61 +227,6 @@ struct Src {
         d7 = *reinterpret_cast<const uint32_t *>(p + 7 * S::ROWB);
     }
 
-    // Epilogue for output rows Y0..Y0+NR-1 of this part (decode only): acc ^= the received
-    // recovery block of generator row y (zeros when absent). Loaded as 16-byte items (sub-block
-    // b, 4-column chunk t; item i = lane + 64h: b = i / 16, t = i % 16, the store layout of Sink)
-    // with buffer_load_dwordx4 and transposed back to one word per lane through the wave's LDS
-    // scratch: 2 load instructions per row instead of 8, all loads of 4 rows in flight together.
-    uint32_t cbase[2];        // decode epilogue: item chunk base (block 0 of the chunk's group)
-    int cgl;                  // decode epilogue: the item chunk's group (position-table index)
-    uint8_t *scr;             // this wave's LDS scratch [8][64] words
-    int lane;
-
-    __device__ __forceinline__ void init_items(const FixedArgs &a, const WGInfo &w, uint8_t *scratch) {
-        const Geometry &geo = a.geo;
-        scr = scratch;
-        lane = w.lane;
-        const int t = w.lane & 15;
-        const long long colx = w.col0 + (w.c - w.lane) + 4 * t;
-        const int gx = colx >= 0 ? static_cast<int>(colx / geo.nq) : -1;
-        const int qx = static_cast<int>(colx - static_cast<long long>(gx) * geo.nq);
-        const bool ok = colx >= w.lo && colx < w.hi;
-        cgl = ok ? gx - w.g_first : 0;
-        const uint32_t base = static_cast<uint32_t>(cgl) * static_cast<uint32_t>(a.in_gstride) + col_off(qx, geo);
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-            cbase[h] = ok ? base + static_cast<uint32_t>((w.lane >> 4) + 4 * h) * geo.sub : OOR;
-    }
-
-    template <int Y0, int NR>
-    __device__ __forceinline__ void epilogue(uint32_t (&acc)[NR][8]) const {
-        if (!DEC) return;
-        constexpr int CH = 4;  // rows per batch of loads (register budget: 8 x 4 VGPRs)
-#pragma unroll
-        for (int y0 = 0; y0 < NR; y0 += CH) {
-            u32x4 v[CH][2];
-#pragma unroll
-            for (int yi = 0; yi < CH && y0 + yi < NR; ++yi) {
-                const int p = pos[cgl * (S::KP + S::MP) + S::KP + Y0 + y0 + yi];
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const uint32_t o = (p == 0xFF || cbase[h] == OOR) ? OOR : cbase[h] + static_cast<uint32_t>(p) * B;
-                    v[yi][h] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, 0, 0);
-                }
-            }
-#pragma unroll
-            for (int yi = 0; yi < CH && y0 + yi < NR; ++yi) {
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int i = lane + 64 * h;
-                    *reinterpret_cast<u32x4 *>(scr + (i >> 4) * 256 + (i & 15) * 16) = v[yi][h];
-                }
-#pragma unroll
-                for (int aa = 0; aa < 8; ++aa)
-                    acc[y0 + yi][aa] = X2(acc[y0 + yi][aa], reinterpret_cast<const uint32_t *>(scr)[aa * 64 + lane]);
-            }
-        }
-    }
 };
 
 // Output, transposed through a per-wave 2 KB LDS scratch so every store is 16 contiguous bytes:
@@ -349,7 +299,7 @@ struct Sink {
 };
 
 // Sets up src/sink for the tile starting at column col0 (columns outside [lo, hi) are idle
-// lanes), issues the ring's first R-1 DMAs and returns this wave's part. The caller (the FIXED_KERNEL macro)
+// lanes) and returns this wave's part. The caller (the FIXED_KERNEL macro)
 // then calls the generated run_<name> directly, so everything inlines into one function: a
 // non-inlined body took `src` by reference through scratch and read the LDS ring with flat loads.
 template <class S, bool DEC>
@@ -393,13 +343,8 @@ __device__ __forceinline__ int kernel_prologue(const FixedArgs &a, uint8_t *lds,
         __syncthreads();
     }
     src.init(a, w, lds, lds_pos);
-    if (DEC) src.init_items(a, w, lds + w.wave * 2048);
     sink.init(a, w, lds + w.wave * 2048);
-    if (S::DMA) {
-#pragma unroll
-        for (int x = 0; x < S::R - 1 && x < S::K; ++x) src.issue(x, src.pre(x));
-    }
-    return part;
+    return part;  // the generated body issues the ring's first DMAs
 }
 
 // XCD-aware tile order. Workgroups are dealt round-robin over the 8 XCDs (block b -> XCD b % 8;
@@ -446,7 +391,7 @@ inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArg
         const long long c0 = static_cast<long long>(xcd_tile(blockIdx.x, gridDim.x)) * S::COLS;  \
         const int part = kernel_prologue<S, DEC>(a, lds, src, sink, c0, 0,                       \
                                                  static_cast<long long>(a.groups) * a.geo.nq);   \
-        run_##NAME(part, src, sink);                                                              \
+        run_##NAME##_##MODE(part, src, sink);                                                     \
     }                                                                                             \
     hipError_t launch_##NAME##_##MODE(FixedArgs a, hipStream_t s) {                               \
         return launch_shape<Shape<K, M, P, CW, R, DMA>, DEC>(a, s, kern_##NAME##_##MODE);         \

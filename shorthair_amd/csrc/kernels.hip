@@ -359,9 +359,15 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
     uint64_t *Tg = fixed_mode ? a.targets + static_cast<long long>(g) * emax * a.ldB : nullptr;
     const uint64_t tnull = a.snip_base + static_cast<uint64_t>(SNIP_NULL) * SNIP_STRIDE;
     if (fixed_mode) {
+        // every address stage B reads is written exactly once: (i < e, j < e) by put() below,
+        // the unused outputs j in [e, ldB) here
         uint8_t *rr = a.rrow + static_cast<long long>(g) * a.ldR;
         for (int i = lane; i < e; i += 64) rr[i] = s_rrow[i];
-        for (int t = lane; t < emax * a.ldB; t += 64) Tg[t] = tnull;
+        const int pad = a.ldB - e;
+        for (int t = lane; t < e * pad; t += 64) {
+            const int i = t / pad, j = e + (t - i * pad);
+            Tg[(static_cast<long long>(j >> 3) * emax + i) * 8 + (j & 7)] = tnull;
+        }
     } else {
         for (int t = lane; t < emax * a.ldB; t += 64) Bc[t] = 0;
     }

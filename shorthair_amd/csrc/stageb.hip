@@ -278,19 +278,19 @@ __global__ __launch_bounds__(256, 4) void stageb_fixed(StageBFixedArgs a) {
     if (e > 1) load_row(1, r1);
     int i = 0;
     for (; i + 3 <= e; i += 3) {  // rows i, i+1, i+2 in r0, r1, r2 (rotating, two rows in flight)
-        uint64_t tg[8];
+        // the three rows' snippet addresses in one batch of scalar loads: scalar loads return
+        // out of order, so any wait for one of them waits for all (one exposed latency per 3 rows)
+        uint64_t tg[3][8];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) tg[r][j] = tp[(i + r) * 8 + j];
         if (i + 2 < e) load_row(i + 2, r2);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) tg[j] = tp[i * 8 + j];
-        row_regs(r0, tg, a01, a23, a45, a67, z0, z1);
+        row_regs(r0, tg[0], a01, a23, a45, a67, z0, z1);
         if (i + 3 < e) load_row(i + 3, r0);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) tg[j] = tp[(i + 1) * 8 + j];
-        row_regs(r1, tg, a01, a23, a45, a67, z0, z1);
+        row_regs(r1, tg[1], a01, a23, a45, a67, z0, z1);
         if (i + 4 < e) load_row(i + 4, r1);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) tg[j] = tp[(i + 2) * 8 + j];
-        row_regs(r2, tg, a01, a23, a45, a67, z0, z1);
+        row_regs(r2, tg[2], a01, a23, a45, a67, z0, z1);
     }
     if (i < e) {  // one or two rows left, in r0 (and r1)
         uint64_t tg[8];

@@ -13,7 +13,8 @@ chains spanning all k steps are reassociated by LLVM into trees that keep every 
 
 One generated kernel serves two modes (template flag DEC):
   encode       recovery[g][y] = sum_x M(C[y][x]) data[g][x]             (y < m, row 0 = ones)
-  decode A     residual[g][y] = R_y + sum_{x received} M(C[y][x]) d_x   (erased x read as zeros)
+  decode A     residual[g][y] = R_y + sum_{x received} M(C[y][x]) d_x   (erased x read as zeros;
+               R_y streamed through the same ring as m extra steps after the k input steps)
 Rows are split into parts of <= 16 rows (128 accumulator VGPRs); the waves of one workgroup
 run the parts of the same columns, so the second part's loads hit L1/L2.
 
@@ -131,43 +132,65 @@ class Body:
         have.add(name)
         return name
 
-    def emit(self, R, S):
-        """Software-pipelined steps (see fixed_common.hpp): iteration x waits for slot x+1,
-        reads it into the other register set, refills slot x-1 with block x+R-1, and computes
-        step x from the registers read one iteration earlier. Sets alternate: dA (even x), dB."""
+    def emit(self, R, S, steps, KP):
+        """Software-pipelined steps (see fixed_common.hpp): step i waits for slot i+1, reads it
+        into the other register set, refills freed slots up to step i+R-1, and computes step i
+        from the registers read one iteration earlier. Sets alternate: dA (even i), dB.
+        steps: ("c", x) = input column x (position-table entry x), ("r", y) = decode only: the
+        received recovery block of generator row y (entry KP + y), added to row y's residual."""
         L = self.lines
         nr = self.y1 - self.y0
-        k = self.k
+        n = len(steps)
+        dma = "nodma" not in ABLATE
+
+        def tidx(st):
+            return st[1] if st[0] == "c" else KP + st[1]
+
+        def uses(st):
+            return st[0] == "c" or self.y0 <= st[1] < self.y1
+
         L.append("    uint32_t dA0, dA1, dA2, dA3, dA4, dA5, dA6, dA7;")
         L.append("    uint32_t dB0, dB1, dB2, dB3, dB4, dB5, dB6, dB7;")
-        # prologue: steps 0..R-2 were issued by kernel_prologue; wait for the first group
-        nxt_issue = min(k, R - 1)  # steps 0..nxt_issue-1 issued (in order)
-        L.append(f"    src.template wait<{min(k, S) - 1}, {nxt_issue}>();")
-        L.append("    src.read(0, " + ", ".join(f"dA{a}" for a in range(8)) + ");")
-        if nxt_issue < k:
-            L.append(f"    typename Src::Pre pre = src.pre({nxt_issue});")
-        for x in range(k):
-            cur, nxt = ("dA", "dB") if x % 2 == 0 else ("dB", "dA")
-            L.append(f"    // ---- input block {x}")
+        nxt_issue = min(n, R - 1)  # steps 0..nxt_issue-1 issued (in order)
+        if dma:
+            for t in range(nxt_issue):
+                L.append(f"    src.issue({t}, src.pre({tidx(steps[t])}));")
+        L.append(f"    src.template wait<{min(n, S) - 1}, {nxt_issue}>();")
+        if uses(steps[0]):
+            L.append("    src.read(0, " + ", ".join(f"dA{a}" for a in range(8)) + ");")
+        if nxt_issue < n:
+            L.append(f"    typename Src::Pre pre = src.pre({tidx(steps[nxt_issue])});")
+        for i, st in enumerate(steps):
+            cur, nxt = ("dA", "dB") if i % 2 == 0 else ("dB", "dA")
+            L.append(f"    // ---- step {i}: " + (f"input block {st[1]}" if st[0] == "c" else f"recovery row {st[1]}"))
             # Pin the step structure: without this hipcc hoists work across steps.
             L.append("    __builtin_amdgcn_sched_barrier(0);")
-            if x + 1 < k:
-                if (x + 1) % S == 0:
-                    # group boundary: the next S blocks must have landed (counted vmcnt) and every
-                    # wave must be past block x-1 (barrier), which frees the slots of blocks <= x-1
+            if i + 1 < n:
+                if (i + 1) % S == 0:
+                    # group boundary: the next S steps must have landed (counted vmcnt) and every
+                    # wave must be past step i-1 (barrier), which frees the slots of steps <= i-1
                     if "nobar" not in ABLATE:
-                        L.append(f"    src.template wait<{min(k - 1, x + S)}, {nxt_issue}>();")
-                    while nxt_issue < k and nxt_issue - R <= x - 1:
-                        if "nodma" not in ABLATE:
+                        L.append(f"    src.template wait<{min(n - 1, i + S)}, {nxt_issue}>();")
+                    while nxt_issue < n and nxt_issue - R <= i - 1:
+                        if dma:
                             L.append(f"    src.issue({nxt_issue}, pre);")
                         nxt_issue += 1
-                        if nxt_issue < k:
-                            L.append(f"    pre = src.pre({nxt_issue});")
-                L.append(f"    src.read({(x + 1) % R}, " + ", ".join(f"{nxt}{a}" for a in range(8)) + ");")
-                if READ_PIN:
-                    # keep the next block's ds_reads at the top of the step: left free, the
-                    # scheduler sinks them to ~25 VALU before their use (LDS latency exposed)
-                    L.append("    __builtin_amdgcn_sched_barrier(0);")
+                        if nxt_issue < n:
+                            L.append(f"    pre = src.pre({tidx(steps[nxt_issue])});")
+                if uses(steps[i + 1]):
+                    L.append(f"    src.read({(i + 1) % R}, " + ", ".join(f"{nxt}{a}" for a in range(8)) + ");")
+                    if READ_PIN:
+                        # keep the next block's ds_reads at the top of the step: left free, the
+                        # scheduler sinks them to ~25 VALU before their use (LDS latency exposed)
+                        L.append("    __builtin_amdgcn_sched_barrier(0);")
+            if st[0] == "r":
+                if uses(st):  # residual row y += the received recovery block R_y (zeros if absent)
+                    yi = st[1] - self.y0
+                    for b in range(8):
+                        L.append(f"    XV(acc[{yi}][{b}], {cur}{b});")
+                    L.append(f"    PIN8(acc[{yi}]);")
+                continue
+            x = st[1]
             L.append("    {")
             have = set()
             # Updates ordered by the high-half table entry: each T1 entry is built right before
@@ -244,38 +267,41 @@ def gen_config(k, m):
            "namespace sh {",
            "namespace fixed {",
            ""]
-    for p, (y0, y1) in enumerate(parts):
-        body = Body(k, rows, y0, y1).emit(R, sync)
-        nr = y1 - y0
-        out.append(f"template <class Src>")
-        out.append(f"__device__ __forceinline__ void run_{name}_p{p}(const Src &src, const Sink &sink) {{")
-        out.append(f"    uint32_t acc[{nr}][8];")
-        # opaque zeros: a constant 0 would be folded into the first step, whose pinned results
-        # then need register copies of shared table entries (AGPR spills at k=200).
-        out.append(f"    for (int y = 0; y < {nr}; ++y) for (int b = 0; b < 8; ++b) ZERO(acc[y][b]);")
-        out.append(body)
-        out.append("    __builtin_amdgcn_sched_barrier(0);")
-        out.append(f"    // epilogue: (decode) + received recovery rows, end fix-up, store rows {y0}..{y1 - 1}")
-        out.append("    src.release();  // the store scratch aliases the ring")
-        out.append(f"    src.template epilogue<{y0}, {nr}>(acc);")
-        for yi in range(nr):
+    KP = (k + 3) & ~3
+    for mode in ("enc", "dec"):
+        steps = [("c", x) for x in range(k)] + ([("r", y) for y in range(m)] if mode == "dec" else [])
+        for p, (y0, y1) in enumerate(parts):
+            body = Body(k, rows, y0, y1).emit(R, sync, steps, KP)
+            nr = y1 - y0
+            out.append(f"template <class Src>")
+            out.append(f"__device__ __forceinline__ void run_{name}_{mode}_p{p}(const Src &src, const Sink &sink) {{")
+            out.append(f"    uint32_t acc[{nr}][8];")
+            # opaque zeros: a constant 0 would be folded into the first step, whose pinned results
+            # then need register copies of shared table entries (AGPR spills at k=200).
+            out.append(f"    for (int y = 0; y < {nr}; ++y) for (int b = 0; b < 8; ++b) ZERO(acc[y][b]);")
+            out.append(body)
             out.append("    __builtin_amdgcn_sched_barrier(0);")
-            if "halfstore" in ABLATE and p >= len(parts) // 2:
-                out.append(f"    asm volatile(\"\" :: " + ", ".join(f'"v"(acc[{yi}][{b}])' for b in range(8)) + ");")
-            elif os.environ.get("SH_GEN_STORE") == "1":
-                out.append(f"    sink.store_row_dw({y0 + yi}, acc[{yi}]);")
-            elif "nostore" in ABLATE:
-                out.append(f"    asm volatile(\"\" :: " + ", ".join(f'"v"(acc[{yi}][{b}])' for b in range(8)) + ");")
-            else:
-                out.append(f"    sink.store_row({y0 + yi}, acc[{yi}]);")
+            out.append(f"    // epilogue: store rows {y0}..{y1 - 1}")
+            out.append("    src.release();  // the store scratch aliases the ring")
+            for yi in range(nr):
+                out.append("    __builtin_amdgcn_sched_barrier(0);")
+                if "halfstore" in ABLATE and p >= len(parts) // 2:
+                    out.append(f"    asm volatile(\"\" :: " + ", ".join(f'"v"(acc[{yi}][{b}])' for b in range(8)) + ");")
+                elif os.environ.get("SH_GEN_STORE") == "1":
+                    out.append(f"    sink.store_row_dw({y0 + yi}, acc[{yi}]);")
+                elif "nostore" in ABLATE:
+                    out.append(f"    asm volatile(\"\" :: " + ", ".join(f'"v"(acc[{yi}][{b}])' for b in range(8)) + ");")
+                else:
+                    out.append(f"    sink.store_row({y0 + yi}, acc[{yi}]);")
+            out.append("}")
+            out.append("")
+        out.append(f"template <class Src>")
+        out.append(f"__device__ __forceinline__ void run_{name}_{mode}(int part, const Src &src, const Sink &sink) {{")
+        for p in range(len(parts)):
+            kw = "if" if p == 0 else "else if"
+            out.append(f"    {kw} (part == {p}) run_{name}_{mode}_p{p}(src, sink);")
         out.append("}")
         out.append("")
-    out.append(f"template <class Src>")
-    out.append(f"__device__ __forceinline__ void run_{name}(int part, const Src &src, const Sink &sink) {{")
-    for p in range(len(parts)):
-        kw = "if" if p == 0 else "else if"
-        out.append(f"    {kw} (part == {p}) run_{name}_p{p}(src, sink);")
-    out.append("}")
     out.append("}  // namespace fixed")
     out.append("}  // namespace sh")
     os.makedirs(OUTDIR, exist_ok=True)
