@@ -263,8 +263,13 @@ __global__ __launch_bounds__(256, 4) void stageb_fixed(StageBFixedArgs a) {
     typedef const __attribute__((address_space(4))) uint64_t cu64_t;
     const cu32_t *rr = (const cu32_t *)(a.rrow + static_cast<long long>(g) * a.ldR);  // ldR % 4 == 0
     const cu64_t *tp = (const cu64_t *)(a.targets + (static_cast<long long>(g) * (a.ldT / 8) + (j0 >> 3)) * a.emax * 8);
-    auto load_row = [&](int i, Row8 &d) {
-        const uint32_t soff = ((rr[i >> 2] >> (8 * (i & 3))) & 0xFFu) * static_cast<uint32_t>(geo.B);
+    const int elast = e - 1;
+    auto row_of = [&](int i) { return min(i, elast); };  // prefetches past the end re-read the last row
+    auto row_soff = [&](int i) {
+        i = row_of(i);
+        return ((rr[i >> 2] >> (8 * (i & 3))) & 0xFFu) * static_cast<uint32_t>(geo.B);
+    };
+    auto load_row = [&](uint32_t soff, Row8 &d) {
 #pragma unroll
         for (int s = 0; s < 8; ++s) d.w[s] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff[s], soff, 0);
     };
@@ -274,32 +279,40 @@ __global__ __launch_bounds__(256, 4) void stageb_fixed(StageBFixedArgs a) {
     for (int t = 0; t < 16; ++t) a01[t] = a23[t] = a45[t] = a67[t] = 0;
     uint32_t z0 = 0, z1 = 0;
     Row8 r0, r1, r2;
-    load_row(0, r0);
-    if (e > 1) load_row(1, r1);
+    load_row(row_soff(0), r0);
+    load_row(row_soff(1), r1);
     int i = 0;
     for (; i + 3 <= e; i += 3) {  // rows i, i+1, i+2 in r0, r1, r2 (rotating, two rows in flight)
-        // the three rows' snippet addresses in one batch of scalar loads: scalar loads return
-        // out of order, so any wait for one of them waits for all (one exposed latency per 3 rows)
+        // the three rows' snippet addresses and the next three row offsets in one batch of scalar
+        // loads: scalar loads return out of order, so any wait for one of them waits for all
+        // (one exposed latency per 3 rows). The row loads are unconditional (indices clamped to
+        // the last row, re-reads are L2 hits) so the counted vmcnt waits stay two rows deep.
+        const int i2 = row_of(i + 2), i3 = row_of(i + 3), i4 = row_of(i + 4);
+        const uint32_t w2 = rr[i2 >> 2], w3 = rr[i3 >> 2], w4 = rr[i4 >> 2];
         uint64_t tg[3][8];
 #pragma unroll
-        for (int r = 0; r < 3; ++r)
+        for (int r = 0; r < 3; ++r) {
+            const int x = row_of(i + r);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) tg[r][j] = tp[(i + r) * 8 + j];
-        if (i + 2 < e) load_row(i + 2, r2);
+            for (int j = 0; j < 8; ++j) tg[r][j] = tp[x * 8 + j];
+        }
+        auto pick = [&](uint32_t w, int x) { return ((w >> (8 * (x & 3))) & 0xFFu) * static_cast<uint32_t>(geo.B); };
+        const uint32_t s2 = pick(w2, i2), s3 = pick(w3, i3), s4 = pick(w4, i4);
+        load_row(s2, r2);
         row_regs(r0, tg[0], a01, a23, a45, a67, z0, z1);
-        if (i + 3 < e) load_row(i + 3, r0);
+        load_row(s3, r0);
         row_regs(r1, tg[1], a01, a23, a45, a67, z0, z1);
-        if (i + 4 < e) load_row(i + 4, r1);
+        load_row(s4, r1);
         row_regs(r2, tg[2], a01, a23, a45, a67, z0, z1);
     }
     if (i < e) {  // one or two rows left, in r0 (and r1)
         uint64_t tg[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) tg[j] = tp[i * 8 + j];
+        for (int j = 0; j < 8; ++j) tg[j] = tp[row_of(i) * 8 + j];
         row_regs(r0, tg, a01, a23, a45, a67, z0, z1);
         if (i + 1 < e) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) tg[j] = tp[(i + 1) * 8 + j];
+            for (int j = 0; j < 8; ++j) tg[j] = tp[row_of(i + 1) * 8 + j];
             row_regs(r1, tg, a01, a23, a45, a67, z0, z1);
         }
     }

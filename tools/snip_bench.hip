@@ -5,6 +5,8 @@
 //   call   s_swappc into the accumulating snippet of the coefficient (VGPR-index mode), as
 //          stageb_fixed does (2 redirects per product)
 //   inline the same 8 bitop3 per product inline for a fixed coefficient (no redirect): the floor
+//   index  no redirect: per output bit two v_xor_b32 whose SRC0 is VGPR-indexed into the tables
+//          (s_set_gpr_idx_idx per lookup, indices packed 4 per SGPR as lo, 16+hi)
 //   chain  threaded dispatch: the caller jumps into the first snippet; every snippet returns to a
 //          per-position trampoline that selects the next accumulator set and jumps on
 //          (still 2 redirects, measured against "call" for the trampoline cost)
@@ -63,6 +65,16 @@ __global__ void snip_table_holder(uint64_t *out) {
     if (threadIdx.x == 0) *out = base;
 }
 
+// MODE 2: one index dword D holds the 4 lookups of bits (b, b+1) as bytes lo, 16+hi, lo, 16+hi;
+// each lookup is s_set_gpr_idx_idx + one v_xor_b32 whose SRC0 (v96 = table base) is indexed.
+#define IX_DW(D, A, B)                                                                            \
+    "s_set_gpr_idx_idx %[" D "]\n v_xor_b32 v" A ", v96, v" A "\n"                                \
+    "s_lshr_b32 s90, %[" D "], 8\n s_set_gpr_idx_idx s90\n v_xor_b32 v" A ", v96, v" A "\n"      \
+    "s_lshr_b32 s90, %[" D "], 16\n s_set_gpr_idx_idx s90\n v_xor_b32 v" B ", v96, v" B "\n"     \
+    "s_lshr_b32 s90, %[" D "], 24\n s_set_gpr_idx_idx s90\n v_xor_b32 v" B ", v96, v" B "\n"
+#define IX_OUT(J, A0, A1, A2, A3, A4, A5, A6, A7)                                                 \
+    IX_DW("x" #J "a", A0, A1) IX_DW("x" #J "b", A2, A3) IX_DW("x" #J "c", A4, A5) IX_DW("x" #J "d", A6, A7)
+
 template <int MODE>
 __global__ __launch_bounds__(256) void bench(const uint64_t *targets, uint32_t *sink, int rows) {
     extern __shared__ uint8_t lds[];
@@ -76,6 +88,8 @@ __global__ __launch_bounds__(256) void bench(const uint64_t *targets, uint32_t *
              d6 = lane * 17, d7 = lane * 19;
     typedef const __attribute__((address_space(4))) uint64_t cu64_t;
     const cu64_t *tp = (const cu64_t *)targets;
+    typedef const __attribute__((address_space(4))) uint32_t cu32_t;
+    const cu32_t *ip = (const cu32_t *)(targets + 64 * 8);
     for (int r = 0; r < rows; ++r) {
         uint64_t tg[8];
         for (int j = 0; j < 8; ++j) tg[j] = tp[((r + blockIdx.x + wave) & 63) * 8 + j];
@@ -182,6 +196,28 @@ __global__ __launch_bounds__(256) void bench(const uint64_t *targets, uint32_t *
                   [d6] "v"(d6), [d7] "v"(d7), "s"(tg[0]), "s"(tg[1]), "s"(tg[2]), "s"(tg[3]), "s"(tg[4]),
                   "s"(tg[5]), "s"(tg[6]), "s"(tg[7])
                 : CLOBBERS);
+        } else if (MODE == 2) {
+            uint32_t ix[32];
+            for (int j = 0; j < 32; ++j) ix[j] = ip[((r + blockIdx.x + wave) & 63) * 32 + j];
+            asm volatile(
+                "v_mov_b32 v97, %[d0]\n v_mov_b32 v98, %[d1]\n v_mov_b32 v100, %[d2]\n v_mov_b32 v104, %[d3]\n"
+                "v_mov_b32 v113, %[d4]\n v_mov_b32 v114, %[d5]\n v_mov_b32 v116, %[d6]\n v_mov_b32 v120, %[d7]\n"
+                TABLES
+                "s_set_gpr_idx_on 0, gpr_idx(SRC0)\n"
+                IX_OUT(0, "32", "33", "34", "35", "36", "37", "38", "39")
+                IX_OUT(1, "40", "41", "42", "43", "44", "45", "46", "47")
+                IX_OUT(2, "48", "49", "50", "51", "52", "53", "54", "55")
+                IX_OUT(3, "56", "57", "58", "59", "60", "61", "62", "63")
+                IX_OUT(4, "64", "65", "66", "67", "68", "69", "70", "71")
+                IX_OUT(5, "72", "73", "74", "75", "76", "77", "78", "79")
+                IX_OUT(6, "80", "81", "82", "83", "84", "85", "86", "87")
+                IX_OUT(7, "88", "89", "90", "91", "92", "93", "94", "95")
+                "s_set_gpr_idx_off"
+                : "+{v[32:47]}"(a01), "+{v[48:63]}"(a23), "+{v[64:79]}"(a45), "+{v[80:95]}"(a67),
+                  "+{v96}"(z0), "+{v112}"(z1)
+                : [d0] "v"(d0), [d1] "v"(d1), [d2] "v"(d2), [d3] "v"(d3), [d4] "v"(d4), [d5] "v"(d5),
+                  [d6] "v"(d6), [d7] "v"(d7), [x0a] "s"(ix[0]), [x0b] "s"(ix[1]), [x0c] "s"(ix[2]), [x0d] "s"(ix[3]), [x1a] "s"(ix[4]), [x1b] "s"(ix[5]), [x1c] "s"(ix[6]), [x1d] "s"(ix[7]), [x2a] "s"(ix[8]), [x2b] "s"(ix[9]), [x2c] "s"(ix[10]), [x2d] "s"(ix[11]), [x3a] "s"(ix[12]), [x3b] "s"(ix[13]), [x3c] "s"(ix[14]), [x3d] "s"(ix[15]), [x4a] "s"(ix[16]), [x4b] "s"(ix[17]), [x4c] "s"(ix[18]), [x4d] "s"(ix[19]), [x5a] "s"(ix[20]), [x5b] "s"(ix[21]), [x5c] "s"(ix[22]), [x5d] "s"(ix[23]), [x6a] "s"(ix[24]), [x6b] "s"(ix[25]), [x6c] "s"(ix[26]), [x6d] "s"(ix[27]), [x7a] "s"(ix[28]), [x7b] "s"(ix[29]), [x7c] "s"(ix[30]), [x7d] "s"(ix[31])
+                : CLOBBERS, "s90", "scc");
         }
         d0 += a01[r & 15];
     }
@@ -199,9 +235,12 @@ int main(int argc, char **argv) {
     hipMalloc(&d_base, 8);
     hipLaunchKernelGGL(snip_table_holder, dim3(1), dim3(64), 0, 0, d_base);
     hipMemcpy(&base, d_base, 8, hipMemcpyDeviceToHost);
-    uint64_t h[64 * 8];
+    uint64_t h[64 * 8 + 64 * 16];  // snippet targets, then MODE 2 index dwords (64 rows x 32)
     srand(7);
     for (int i = 0; i < 64 * 8; ++i) h[i] = base + (uint64_t)(1 + rand() % 255) * SH_SNIPA_STRIDE;
+    uint32_t *ixs = (uint32_t *)(h + 64 * 8);
+    for (int i = 0; i < 64 * 32; ++i)  // bytes: lo, 16 + hi, lo, 16 + hi
+        ixs[i] = (rand() & 15) | ((16 + (rand() & 15)) << 8) | ((rand() & 15) << 16) | ((16 + (rand() & 15)) << 24);
     uint64_t *d_t;
     uint32_t *d_sink;
     hipMalloc(&d_t, sizeof h);
@@ -212,7 +251,8 @@ int main(int argc, char **argv) {
     hipEventCreate(&e1);
     auto go = [&]() {
         if (mode == 0) hipLaunchKernelGGL(bench<0>, dim3(nwg), dim3(256), ldsb, 0, d_t, d_sink, rows);
-        else hipLaunchKernelGGL(bench<1>, dim3(nwg), dim3(256), ldsb, 0, d_t, d_sink, rows);
+        else if (mode == 1) hipLaunchKernelGGL(bench<1>, dim3(nwg), dim3(256), ldsb, 0, d_t, d_sink, rows);
+        else hipLaunchKernelGGL(bench<2>, dim3(nwg), dim3(256), ldsb, 0, d_t, d_sink, rows);
     };
     go();
     hipDeviceSynchronize();
@@ -226,7 +266,7 @@ int main(int argc, char **argv) {
     ms /= it;
     const double products = (double)nwg * 4 * rows * 8;
     printf("mode=%s nwg=%d lds=%d rows=%d: %.4f ms, %.2f G wave-products/s, %.1f ns per wave-product per CU\n",
-           mode == 0 ? "call" : "inline", nwg, ldsb, rows, ms, products / ms / 1e6, ms * 1e6 * 256 / products);
+           mode == 0 ? "call" : mode == 1 ? "inline" : "index", nwg, ldsb, rows, ms, products / ms / 1e6, ms * 1e6 * 256 / products);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) printf("error %s\n", hipGetErrorString(err));
     return 0;
