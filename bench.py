@@ -351,11 +351,12 @@ def _time_ops(args, sh, torch, s, k, m, B, G, data, rec, e_fixed, encode=True, i
     return r
 
 
-def pmc_traffic(sh, mode, k, m, B, G, e):
-    """HBM bytes per launch of the dominant kernel from the committed PMC summary
-    (profiles/*/traffic*.json, written by tools/gpu_traffic.sh: FETCH_SIZE and WRITE_SIZE in
-    separate rocprofv3 passes, FETCH_SIZE doubled per the gfx950 correction). Used only when that
-    summary was measured on this very library build (SHA-256) and workload; else None."""
+def pmc_traffic(sh, k, m, B, G, e):
+    """Per-kernel HBM bytes per launch from the committed PMC summary (profiles/*/traffic*.json,
+    written by tools/gpu_traffic.sh: FETCH_SIZE and WRITE_SIZE in separate rocprofv3 passes,
+    FETCH_SIZE doubled per the gfx950 correction). Used only when that summary was measured on
+    this very library build (SHA-256; builds are deterministic, so the driver's rebuild of the
+    same sources matches) and workload; else (None, None)."""
     import glob
     import hashlib
     try:
@@ -363,15 +364,14 @@ def pmc_traffic(sh, mode, k, m, B, G, e):
     except OSError:
         return None, None
     want = {"k": k, "m": m, "block_bytes": B, "groups": G, "erasures": e}
-    name = f"sh::fixed::kern_k{k}_m{m}_{mode}"
     here = os.path.dirname(os.path.abspath(__file__))
     for path in sorted(glob.glob(os.path.join(here, "profiles", "*", "traffic*.json")), reverse=True):
         try:
             t = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if t.get("lib_sha256") == digest and t.get("workload") == want and name in t.get("kernels", {}):
-            return t["kernels"][name]["hbm_bytes"], os.path.relpath(path, here)
+        if t.get("lib_sha256") == digest and t.get("workload") == want:
+            return t.get("kernels", {}), os.path.relpath(path, here)
     return None, None
 
 
@@ -488,8 +488,24 @@ def main():
         kb = G * (k + m) * B  # algorithmic bytes per launch of either compile-time kernel
         a_ms = stages[1]
         dom = (("encode kernel", enc_ms) if not (a_ms > enc_ms) else ("decode stage-A kernel", a_ms))
-        traffic, traffic_src = pmc_traffic(sh, "enc" if dom[0].startswith("encode") else "dec", k, m, B, G,
-                                           args.erasures)
+        pmc, traffic_src = pmc_traffic(sh, k, m, B, G, args.erasures)
+        names = {"encode": f"sh::fixed::kern_k{k}_m{m}_enc", "decode_stageA": f"sh::fixed::kern_k{k}_m{m}_dec",
+                 "decode_stageB": "sh::stageb_fixed"}
+        e_all = int(es.sum())
+        # stage A reads the k received blocks (survivors + recovery rows) and writes m residual
+        # rows, like encode; stage B reads e residual rows and writes e recovered blocks
+        alg = {"encode": kb, "decode_stageA": kb, "decode_stageB": 2 * e_all * B}
+        traffic = None
+        pmc_line = None
+        if pmc:
+            pmc_line = {}
+            for op, nm in names.items():
+                if nm in pmc:
+                    t = pmc[nm]
+                    pmc_line[op] = {"read_bytes": t["read_bytes"], "write_bytes": t["write_bytes"],
+                                    "alg_bytes": alg[op], "traffic_over_alg": round(t["hbm_bytes"] / alg[op], 3)}
+            dom_op = "encode" if dom[0].startswith("encode") else "decode_stageA"
+            traffic = pmc.get(names[dom_op], {}).get("hbm_bytes")
         threads = args.cpu_threads or host_cores()
         cpu = None if args.no_cpu else cpu_baseline(k, m, B, args.erasures, args.cpu_seconds, threads)
         line = {
@@ -519,7 +535,14 @@ def main():
                          "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": round(kb / (dom[1] * 1e-3) / HBM_PEAK, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
+                         "traffic_over_alg": round(traffic / kb, 3) if traffic else None,
                          "alg_bytes_per_launch": kb, "launch_ms": round(dom[1], 4)},
+            "op_roofline": {  # algorithmic bytes / measured time, as a fraction of 8 TB/s
+                "encode": round(enc_bytes / (enc_ms * 1e-3) / HBM_PEAK, 4),
+                "decode": round(dec_bytes / (dec_ms * 1e-3) / HBM_PEAK, 4),
+                "decode_stageA": round(alg["decode_stageA"] / (stages[1] * 1e-3) / HBM_PEAK, 4),
+                "decode_stageB": round(alg["decode_stageB"] / (stages[2] * 1e-3) / HBM_PEAK, 4)},
+            "pmc_traffic": pmc_line,
             "cpu_baseline": cpu,
         }
         if root_res is not None:

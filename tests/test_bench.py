@@ -23,9 +23,12 @@ def test_traffic_lookup_requires_matching_build():
     class Fake:
         LIB_PATH = os.path.join(ROOT, "bench.py")  # any file whose hash no summary carries
 
-    assert bench.pmc_traffic(Fake, "dec", 200, 32, 1400, 8192, 32) == (None, None)
-    t, src = bench.pmc_traffic(sh, "dec", 200, 32, 1400, 8192, 32)
+    assert bench.pmc_traffic(Fake, 200, 32, 1400, 8192, 32) == (None, None)
+    t, src = bench.pmc_traffic(sh, 200, 32, 1400, 8192, 32)
     assert (t is None) == (src is None)
+    if t is not None:  # a summary of this very build: per-kernel read/write/total bytes
+        for v in t.values():
+            assert v["hbm_bytes"] == v["read_bytes"] + v["write_bytes"] > 0
 
 
 @pytest.mark.parametrize("n", [1, 2, 3])
