@@ -38,6 +38,15 @@ if not os.path.exists(LIB_PATH):
     raise ImportError(f"{LIB_PATH} not built: run `python shorthair_amd/build.py` "
                       "(the codec has no CPU fallback)")
 
+# One HIP runtime per process. PyTorch-ROCm ships its own libamdhip64 / libhsa-runtime64 with
+# the same SONAMEs as /opt/rocm's: loaded after torch, the library binds to torch's copies; loaded
+# before, the process gets two HSA runtimes and whichever initialises second sees no GPU
+# (measured on the box: "No HIP GPUs are available" / our -2). So torch, when present, loads
+# first. Callers without torch are unaffected.
+try:
+    import torch  # noqa: F401
+except ImportError:
+    pass
 lib = ctypes.CDLL(LIB_PATH)
 
 

@@ -109,3 +109,16 @@ def test_synthetic_erasure_pattern_matches_oracle(k, m, e_fixed):
         e2, r2 = po.erasure_pattern(g, k, m, 0xBE, e_fixed)
         assert e1 == e2 and (r1 == r2).all()
     assert shorthair_amd.lib.cauchy_256_erasure_pattern(0, 200, 57, 0, 0, None) == -1
+
+
+@pytest.mark.gpu
+def test_package_before_torch_shares_one_hip_runtime():
+    """Importing shorthair_amd before torch must not load a second HIP/HSA runtime (torch ships
+    its own libamdhip64 with the same SONAME): both the library and torch see the GPU."""
+    import subprocess
+    import sys
+    code = ("import shorthair_amd as s; import torch; assert torch.cuda.is_available(); "
+            "assert s.lib.cauchy_256_batch_init(0) == 0; x = torch.ones(4, device='cuda'); "
+            "assert x.sum().item() == 4.0; print('ok')")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-500:]

@@ -331,6 +331,30 @@ SNIP_T0, SNIP_T1, SNIP_TMP = 100, 116, 132
 SNIPA_ACC, SNIPA_T0, SNIPA_T1 = 32, 96, 112
 
 
+# measurement table for 4-output waves (tools/snip_bench.hip): tables right above the accumulators
+SNIPB_REGS = (32, 64, 80)
+
+
+def acc_table(name, A, T0, T1):
+    low = name.lower()
+    t = [f"#define SH_{name}_ACC {A}", f"#define SH_{name}_T0 {T0}", f"#define SH_{name}_T1 {T1}",
+         f"#define SH_{name}_STRIDE 72", f"#define SH_{name}_NULL 256",
+         f'#define SH_{name}_TABLE(SFX) asm volatile("s_branch sh_{low}_end" #SFX "\\n"',
+         '    ".p2align 6\\n"',
+         f'    "sh_{low}_base" #SFX ":\\n"']
+    for c in range(256):
+        v = c
+        for b in range(8):
+            lo, hi = v & 15, v >> 4
+            t.append(f'    "v_bitop3_b32 v{A + b}, v{A + b}, v{T0 + lo}, v{T1 + hi} bitop3:0x96\\n"')
+            v = gmul(v, 2)
+        t.append('    "s_setpc_b64 s[40:41]\\n"')
+        t.append('    "s_nop 0\\n"')
+    t.append('    "s_setpc_b64 s[40:41]\\n"')
+    t.append(f'    "sh_{low}_end" #SFX ":\\n" ::: "memory")')
+    return t
+
+
 def gen_snippets():
     lines = ["// GENERATED by tools/gen_fixed_kernels.py -- do not edit.",
              "// 256 compile-time 'multiply by c' snippets (see csrc/stageb.hip).",
@@ -357,25 +381,13 @@ def gen_snippets():
     # SNIPA_STRIDE = 72 bytes (8 x 8-byte bitop3 + s_setpc + s_nop), so snippet c sits at
     # base + 72*c; entry 256 is the null snippet (zero coefficient / unused output: return at once).
     # The decode setup writes absolute snippet addresses, so the stage-B loop computes no targets.
-    acc = ['#define SH_SNIPA_ACC %d' % SNIPA_ACC, '#define SH_SNIPA_T0 %d' % SNIPA_T0,
-           '#define SH_SNIPA_T1 %d' % SNIPA_T1, '#define SH_SNIPA_STRIDE 72', '#define SH_SNIPA_NULL 256',
-           '#define SH_SNIPA_TABLE(SFX) asm volatile("s_branch sh_snipa_end" #SFX "\\n"',
-           '    ".p2align 6\\n"',
-           '    "sh_snipa_base" #SFX ":\\n"']
-    for c in range(256):
-        v = c
-        for b in range(8):
-            lo, hi = v & 15, v >> 4
-            acc.append(f'    "v_bitop3_b32 v{SNIPA_ACC + b}, v{SNIPA_ACC + b}, v{SNIPA_T0 + lo}, v{SNIPA_T1 + hi} bitop3:0x96\\n"')
-            v = gmul(v, 2)
-        acc.append('    "s_setpc_b64 s[40:41]\\n"')
-        acc.append('    "s_nop 0\\n"')
-    acc.append('    "s_setpc_b64 s[40:41]\\n"')
-    acc.append('    "sh_snipa_end" #SFX ":\\n" ::: "memory")')
+    acc = acc_table("SNIPA", SNIPA_ACC, SNIPA_T0, SNIPA_T1)
+    accb = acc_table("SNIPB", *SNIPB_REGS)
     with open(os.path.join(OUTDIR, "snippets.h"), "w") as f:
         f.write(lines[0] + "\n" + lines[1] + "\n" + lines[2] + "\n" + "\n".join(lines[3:6]) + "\n"
                 + " \\\n".join(lines[6:]) + "\n")
-        f.write("\n".join(acc[:5]) + "\n" + " \\\n".join(acc[5:]) + "\n")
+        for t in (acc, accb):
+            f.write("\n".join(t[:5]) + "\n" + " \\\n".join(t[5:]) + "\n")
 
 
 def main(argv=()):

@@ -5,6 +5,8 @@
 //   call   s_swappc into the accumulating snippet of the coefficient (VGPR-index mode), as
 //          stageb_fixed does (2 redirects per product)
 //   inline the same 8 bitop3 per product inline for a fixed coefficient (no redirect): the floor
+//   call4  as call, 4 outputs per wave (accumulators v[32:63], tables v[64:95]: 5 waves/SIMD,
+//          twice the table builds per product); run with twice the workgroups for equal work
 //   index  no redirect: per output bit two v_xor_b32 whose SRC0 is VGPR-indexed into the tables
 //          (s_set_gpr_idx_idx per lookup, indices packed 4 per SGPR as lo, 16+hi)
 //   chain  threaded dispatch: the caller jumps into the first snippet; every snippet returns to a
@@ -51,6 +53,20 @@ typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
         "v109", "v110", "v111", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120",   \
         "v121", "v122", "v123", "v124", "v125", "v126", "v127", "s40", "s41", "m0", "memory"
 
+__global__ void snip_table_holder_b(uint64_t *out) {
+    SH_SNIPB_TABLE(U);
+    uint64_t base;
+    asm volatile(
+        "s_getpc_b64 s[42:43]\n"
+        "s_add_u32 s42, s42, sh_snipb_baseU@rel32@lo+4\n"
+        "s_addc_u32 s43, s43, sh_snipb_baseU@rel32@hi+12\n"
+        "s_mov_b64 %0, s[42:43]"
+        : "=s"(base)
+        :
+        : "s42", "s43", "scc");
+    if (threadIdx.x == 0) *out = base;
+}
+
 __global__ void snip_table_holder(uint64_t *out) {
     SH_SNIPA_TABLE(T);
     uint64_t base;
@@ -75,8 +91,34 @@ __global__ void snip_table_holder(uint64_t *out) {
 #define IX_OUT(J, A0, A1, A2, A3, A4, A5, A6, A7)                                                 \
     IX_DW("x" #J "a", A0, A1) IX_DW("x" #J "b", A2, A3) IX_DW("x" #J "c", A4, A5) IX_DW("x" #J "d", A6, A7)
 
+// window tables for MODE 3 (SNIPB registers: T0 = v64.., T1 = v80..)
+#define TABLES_B \
+    "v_xor_b32 v67, v65, v66\n" \
+    "v_xor_b32 v83, v81, v82\n" \
+    "v_xor_b32 v69, v65, v68\n" \
+    "v_xor_b32 v85, v81, v84\n" \
+    "v_xor_b32 v70, v66, v68\n" \
+    "v_xor_b32 v86, v82, v84\n" \
+    "v_xor_b32 v73, v65, v72\n" \
+    "v_xor_b32 v89, v81, v88\n" \
+    "v_xor_b32 v74, v66, v72\n" \
+    "v_xor_b32 v90, v82, v88\n" \
+    "v_xor_b32 v76, v68, v72\n" \
+    "v_xor_b32 v92, v84, v88\n" \
+    "v_xor_b32 v71, v67, v68\n" \
+    "v_xor_b32 v87, v83, v84\n" \
+    "v_xor_b32 v75, v67, v72\n" \
+    "v_xor_b32 v91, v83, v88\n" \
+    "v_xor_b32 v77, v69, v72\n" \
+    "v_xor_b32 v93, v85, v88\n" \
+    "v_xor_b32 v78, v70, v72\n" \
+    "v_xor_b32 v94, v86, v88\n" \
+    "v_xor_b32 v79, v71, v72\n" \
+    "v_xor_b32 v95, v87, v88\n"
+
 template <int MODE>
-__global__ __launch_bounds__(256) void bench(const uint64_t *targets, uint32_t *sink, int rows) {
+__global__ __launch_bounds__(256, MODE == 3 ? 5 : 1) void bench(const uint64_t *targets, uint32_t *sink, int rows,
+                                                               uint64_t tbase, uint64_t tbaseb) {
     extern __shared__ uint8_t lds[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -93,6 +135,8 @@ __global__ __launch_bounds__(256) void bench(const uint64_t *targets, uint32_t *
     for (int r = 0; r < rows; ++r) {
         uint64_t tg[8];
         for (int j = 0; j < 8; ++j) tg[j] = tp[((r + blockIdx.x + wave) & 63) * 8 + j];
+        uint64_t tgb[4];
+        for (int j = 0; j < 4; ++j) tgb[j] = tg[j] - tbase + tbaseb;  // same snippet, SNIPB table
         if (MODE == 0) {
             asm volatile(
                 "v_mov_b32 v97, %[d0]\n v_mov_b32 v98, %[d1]\n v_mov_b32 v100, %[d2]\n v_mov_b32 v104, %[d3]\n"
@@ -196,6 +240,26 @@ __global__ __launch_bounds__(256) void bench(const uint64_t *targets, uint32_t *
                   [d6] "v"(d6), [d7] "v"(d7), "s"(tg[0]), "s"(tg[1]), "s"(tg[2]), "s"(tg[3]), "s"(tg[4]),
                   "s"(tg[5]), "s"(tg[6]), "s"(tg[7])
                 : CLOBBERS);
+        } else if (MODE == 3) {  // 4 outputs per wave, SNIPB registers (v[32:95]: 5 waves/SIMD)
+            asm volatile(
+                "v_mov_b32 v65, %[d0]\n v_mov_b32 v66, %[d1]\n v_mov_b32 v68, %[d2]\n v_mov_b32 v72, %[d3]\n"
+                "v_mov_b32 v81, %[d4]\n v_mov_b32 v82, %[d5]\n v_mov_b32 v84, %[d6]\n v_mov_b32 v88, %[d7]\n"
+                TABLES_B
+                "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"
+                "s_swappc_b64 s[40:41], %[g0]\n"
+                "s_set_gpr_idx_idx 8\n"
+                "s_swappc_b64 s[40:41], %[g1]\n"
+                "s_set_gpr_idx_idx 16\n"
+                "s_swappc_b64 s[40:41], %[g2]\n"
+                "s_set_gpr_idx_idx 24\n"
+                "s_swappc_b64 s[40:41], %[g3]\n"
+                "s_set_gpr_idx_off"
+                : "+{v[32:47]}"(a01), "+{v[48:63]}"(a23), "+{v64}"(z0), "+{v80}"(z1)
+                : [d0] "v"(d0), [d1] "v"(d1), [d2] "v"(d2), [d3] "v"(d3), [d4] "v"(d4), [d5] "v"(d5),
+                  [d6] "v"(d6), [d7] "v"(d7), [g0] "s"(tgb[0]), [g1] "s"(tgb[1]), [g2] "s"(tgb[2]), [g3] "s"(tgb[3])
+                : "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77",
+                  "v78", "v79", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91",
+                  "v92", "v93", "v94", "v95", "s40", "s41", "m0", "memory");
         } else if (MODE == 2) {
             uint32_t ix[32];
             for (int j = 0; j < 32; ++j) ix[j] = ip[((r + blockIdx.x + wave) & 63) * 32 + j];
@@ -235,6 +299,9 @@ int main(int argc, char **argv) {
     hipMalloc(&d_base, 8);
     hipLaunchKernelGGL(snip_table_holder, dim3(1), dim3(64), 0, 0, d_base);
     hipMemcpy(&base, d_base, 8, hipMemcpyDeviceToHost);
+    uint64_t baseb;
+    hipLaunchKernelGGL(snip_table_holder_b, dim3(1), dim3(64), 0, 0, d_base);
+    hipMemcpy(&baseb, d_base, 8, hipMemcpyDeviceToHost);
     uint64_t h[64 * 8 + 64 * 16];  // snippet targets, then MODE 2 index dwords (64 rows x 32)
     srand(7);
     for (int i = 0; i < 64 * 8; ++i) h[i] = base + (uint64_t)(1 + rand() % 255) * SH_SNIPA_STRIDE;
@@ -250,9 +317,10 @@ int main(int argc, char **argv) {
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     auto go = [&]() {
-        if (mode == 0) hipLaunchKernelGGL(bench<0>, dim3(nwg), dim3(256), ldsb, 0, d_t, d_sink, rows);
-        else if (mode == 1) hipLaunchKernelGGL(bench<1>, dim3(nwg), dim3(256), ldsb, 0, d_t, d_sink, rows);
-        else hipLaunchKernelGGL(bench<2>, dim3(nwg), dim3(256), ldsb, 0, d_t, d_sink, rows);
+        if (mode == 0) hipLaunchKernelGGL(bench<0>, dim3(nwg), dim3(256), ldsb, 0, d_t, d_sink, rows, base, baseb);
+        else if (mode == 1) hipLaunchKernelGGL(bench<1>, dim3(nwg), dim3(256), ldsb, 0, d_t, d_sink, rows, base, baseb);
+        else if (mode == 2) hipLaunchKernelGGL(bench<2>, dim3(nwg), dim3(256), ldsb, 0, d_t, d_sink, rows, base, baseb);
+        else hipLaunchKernelGGL(bench<3>, dim3(nwg), dim3(256), ldsb, 0, d_t, d_sink, rows, base, baseb);
     };
     go();
     hipDeviceSynchronize();
@@ -264,9 +332,9 @@ int main(int argc, char **argv) {
     float ms = 0;
     hipEventElapsedTime(&ms, e0, e1);
     ms /= it;
-    const double products = (double)nwg * 4 * rows * 8;
+    const double products = (double)nwg * 4 * rows * (mode == 3 ? 4 : 8);  // per-wave outputs
     printf("mode=%s nwg=%d lds=%d rows=%d: %.4f ms, %.2f G wave-products/s, %.1f ns per wave-product per CU\n",
-           mode == 0 ? "call" : mode == 1 ? "inline" : "index", nwg, ldsb, rows, ms, products / ms / 1e6, ms * 1e6 * 256 / products);
+           mode == 0 ? "call" : mode == 1 ? "inline" : mode == 2 ? "index" : "call4", nwg, ldsb, rows, ms, products / ms / 1e6, ms * 1e6 * 256 / products);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) printf("error %s\n", hipGetErrorString(err));
     return 0;
