@@ -353,7 +353,7 @@ def _time_ops(args, sh, torch, s, k, m, B, G, data, rec, e_fixed, encode=True, i
 
 def pmc_traffic(sh, k, m, B, G, e):
     """Per-kernel HBM bytes per launch from the committed PMC summary (profiles/*/traffic*.json,
-    written by tools/gpu_traffic.sh: FETCH_SIZE and WRITE_SIZE in separate rocprofv3 passes,
+    written by tools/gpu_profile.sh: FETCH_SIZE and WRITE_SIZE in separate rocprofv3 passes,
     FETCH_SIZE doubled per the gfx950 correction). Used only when that summary was measured on
     this very library build (SHA-256; builds are deterministic, so the driver's rebuild of the
     same sources matches) and workload; else (None, None)."""
