@@ -335,10 +335,14 @@ SNIPA_ACC, SNIPA_T0, SNIPA_T1 = 32, 96, 112
 SNIPB_REGS = (32, 64, 80)
 
 
-def acc_table(name, A, T0, T1):
+def acc_table(name, A, T0, T1, chain=False):
+    """chain: the snippet advances the VGPR index to the next accumulator set (m0 += 8), shifts the
+    queue of snippet addresses s[44:61] down one pair and jumps to the next one (one redirect per
+    product; the caller puts 8 addresses + its return address in s[44:61])."""
     low = name.lower()
+    stride = 104 if chain else 72
     t = [f"#define SH_{name}_ACC {A}", f"#define SH_{name}_T0 {T0}", f"#define SH_{name}_T1 {T1}",
-         f"#define SH_{name}_STRIDE 72", f"#define SH_{name}_NULL 256",
+         f"#define SH_{name}_STRIDE {stride}", f"#define SH_{name}_NULL 256",
          f'#define SH_{name}_TABLE(SFX) asm volatile("s_branch sh_{low}_end" #SFX "\\n"',
          '    ".p2align 6\\n"',
          f'    "sh_{low}_base" #SFX ":\\n"']
@@ -348,9 +352,21 @@ def acc_table(name, A, T0, T1):
             lo, hi = v & 15, v >> 4
             t.append(f'    "v_bitop3_b32 v{A + b}, v{A + b}, v{T0 + lo}, v{T1 + hi} bitop3:0x96\\n"')
             v = gmul(v, 2)
+        if chain:
+            t.append('    "s_add_u32 m0, m0, 8\\n"')
+            for q in range(8):
+                t.append(f'    "s_mov_b64 s[{44 + 2 * q}:{45 + 2 * q}], s[{46 + 2 * q}:{47 + 2 * q}]\\n"')
+            t.append('    "s_setpc_b64 s[44:45]\\n"')
+        else:
+            t.append('    "s_setpc_b64 s[40:41]\\n"')
+            t.append('    "s_nop 0\\n"')
+    if chain:  # null entry: same queue step, no XOR work
+        t.append('    "s_add_u32 m0, m0, 8\\n"')
+        for q in range(8):
+            t.append(f'    "s_mov_b64 s[{44 + 2 * q}:{45 + 2 * q}], s[{46 + 2 * q}:{47 + 2 * q}]\\n"')
+        t.append('    "s_setpc_b64 s[44:45]\\n"')
+    else:
         t.append('    "s_setpc_b64 s[40:41]\\n"')
-        t.append('    "s_nop 0\\n"')
-    t.append('    "s_setpc_b64 s[40:41]\\n"')
     t.append(f'    "sh_{low}_end" #SFX ":\\n" ::: "memory")')
     return t
 
@@ -383,10 +399,11 @@ def gen_snippets():
     # The decode setup writes absolute snippet addresses, so the stage-B loop computes no targets.
     acc = acc_table("SNIPA", SNIPA_ACC, SNIPA_T0, SNIPA_T1)
     accb = acc_table("SNIPB", *SNIPB_REGS)
+    accc = acc_table("SNIPC", SNIPA_ACC, SNIPA_T0, SNIPA_T1, chain=True)
     with open(os.path.join(OUTDIR, "snippets.h"), "w") as f:
         f.write(lines[0] + "\n" + lines[1] + "\n" + lines[2] + "\n" + "\n".join(lines[3:6]) + "\n"
                 + " \\\n".join(lines[6:]) + "\n")
-        for t in (acc, accb):
+        for t in (acc, accb, accc):
             f.write("\n".join(t[:5]) + "\n" + " \\\n".join(t[5:]) + "\n")
 
 

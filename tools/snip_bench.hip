@@ -7,6 +7,8 @@
 //   inline the same 8 bitop3 per product inline for a fixed coefficient (no redirect): the floor
 //   call4  as call, 4 outputs per wave (accumulators v[32:63], tables v[64:95]: 5 waves/SIMD,
 //          twice the table builds per product); run with twice the workgroups for equal work
+//   chain1 one redirect per product: each snippet advances the index (m0 += 8), shifts the queue of
+//          snippet addresses s[44:61] down one pair and jumps to the next (SNIPC table)
 //   index  no redirect: per output bit two v_xor_b32 whose SRC0 is VGPR-indexed into the tables
 //          (s_set_gpr_idx_idx per lookup, indices packed 4 per SGPR as lo, 16+hi)
 //   chain  threaded dispatch: the caller jumps into the first snippet; every snippet returns to a
@@ -67,6 +69,20 @@ __global__ void snip_table_holder_b(uint64_t *out) {
     if (threadIdx.x == 0) *out = base;
 }
 
+__global__ void snip_table_holder_c(uint64_t *out) {
+    SH_SNIPC_TABLE(V);
+    uint64_t base;
+    asm volatile(
+        "s_getpc_b64 s[42:43]\n"
+        "s_add_u32 s42, s42, sh_snipc_baseV@rel32@lo+4\n"
+        "s_addc_u32 s43, s43, sh_snipc_baseV@rel32@hi+12\n"
+        "s_mov_b64 %0, s[42:43]"
+        : "=s"(base)
+        :
+        : "s42", "s43", "scc");
+    if (threadIdx.x == 0) *out = base;
+}
+
 __global__ void snip_table_holder(uint64_t *out) {
     SH_SNIPA_TABLE(T);
     uint64_t base;
@@ -118,7 +134,7 @@ __global__ void snip_table_holder(uint64_t *out) {
 
 template <int MODE>
 __global__ __launch_bounds__(256, MODE == 3 ? 5 : 1) void bench(const uint64_t *targets, uint32_t *sink, int rows,
-                                                               uint64_t tbase, uint64_t tbaseb) {
+                                                               uint64_t tbase, uint64_t tbaseb, uint64_t tbasec) {
     extern __shared__ uint8_t lds[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -135,8 +151,9 @@ __global__ __launch_bounds__(256, MODE == 3 ? 5 : 1) void bench(const uint64_t *
     for (int r = 0; r < rows; ++r) {
         uint64_t tg[8];
         for (int j = 0; j < 8; ++j) tg[j] = tp[((r + blockIdx.x + wave) & 63) * 8 + j];
-        uint64_t tgb[4];
+        uint64_t tgb[4], tgc[8];
         for (int j = 0; j < 4; ++j) tgb[j] = tg[j] - tbase + tbaseb;  // same snippet, SNIPB table
+        for (int j = 0; j < 8; ++j) tgc[j] = tbasec + (tg[j] - tbase) / SH_SNIPA_STRIDE * SH_SNIPC_STRIDE;
         if (MODE == 0) {
             asm volatile(
                 "v_mov_b32 v97, %[d0]\n v_mov_b32 v98, %[d1]\n v_mov_b32 v100, %[d2]\n v_mov_b32 v104, %[d3]\n"
@@ -240,6 +257,23 @@ __global__ __launch_bounds__(256, MODE == 3 ? 5 : 1) void bench(const uint64_t *
                   [d6] "v"(d6), [d7] "v"(d7), "s"(tg[0]), "s"(tg[1]), "s"(tg[2]), "s"(tg[3]), "s"(tg[4]),
                   "s"(tg[5]), "s"(tg[6]), "s"(tg[7])
                 : CLOBBERS);
+        } else if (MODE == 4) {  // chained snippets (SNIPC): one redirect per product
+            uint64_t c0 = tgc[0], c1 = tgc[1], c2 = tgc[2], c3 = tgc[3], c4 = tgc[4], c5 = tgc[5], c6 = tgc[6],
+                     c7 = tgc[7], rr;
+            asm volatile(
+                "v_mov_b32 v97, %[d0]\n v_mov_b32 v98, %[d1]\n v_mov_b32 v100, %[d2]\n v_mov_b32 v104, %[d3]\n"
+                "v_mov_b32 v113, %[d4]\n v_mov_b32 v114, %[d5]\n v_mov_b32 v116, %[d6]\n v_mov_b32 v120, %[d7]\n"
+                TABLES
+                "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"
+                "s_swappc_b64 s[60:61], s[44:45]\n"
+                "s_set_gpr_idx_off"
+                : "+{v[32:47]}"(a01), "+{v[48:63]}"(a23), "+{v[64:79]}"(a45), "+{v[80:95]}"(a67),
+                  "+{v96}"(z0), "+{v112}"(z1), "+{s[44:45]}"(c0), "+{s[46:47]}"(c1), "+{s[48:49]}"(c2),
+                  "+{s[50:51]}"(c3), "+{s[52:53]}"(c4), "+{s[54:55]}"(c5), "+{s[56:57]}"(c6), "+{s[58:59]}"(c7),
+                  "={s[60:61]}"(rr)
+                : [d0] "v"(d0), [d1] "v"(d1), [d2] "v"(d2), [d3] "v"(d3), [d4] "v"(d4), [d5] "v"(d5),
+                  [d6] "v"(d6), [d7] "v"(d7)
+                : CLOBBERS, "scc");
         } else if (MODE == 3) {  // 4 outputs per wave, SNIPB registers (v[32:95]: 5 waves/SIMD)
             asm volatile(
                 "v_mov_b32 v65, %[d0]\n v_mov_b32 v66, %[d1]\n v_mov_b32 v68, %[d2]\n v_mov_b32 v72, %[d3]\n"
@@ -302,6 +336,9 @@ int main(int argc, char **argv) {
     uint64_t baseb;
     hipLaunchKernelGGL(snip_table_holder_b, dim3(1), dim3(64), 0, 0, d_base);
     hipMemcpy(&baseb, d_base, 8, hipMemcpyDeviceToHost);
+    uint64_t basec;
+    hipLaunchKernelGGL(snip_table_holder_c, dim3(1), dim3(64), 0, 0, d_base);
+    hipMemcpy(&basec, d_base, 8, hipMemcpyDeviceToHost);
     uint64_t h[64 * 8 + 64 * 16];  // snippet targets, then MODE 2 index dwords (64 rows x 32)
     srand(7);
     for (int i = 0; i < 64 * 8; ++i) h[i] = base + (uint64_t)(1 + rand() % 255) * SH_SNIPA_STRIDE;
@@ -317,10 +354,11 @@ int main(int argc, char **argv) {
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     auto go = [&]() {
-        if (mode == 0) hipLaunchKernelGGL(bench<0>, dim3(nwg), dim3(256), ldsb, 0, d_t, d_sink, rows, base, baseb);
-        else if (mode == 1) hipLaunchKernelGGL(bench<1>, dim3(nwg), dim3(256), ldsb, 0, d_t, d_sink, rows, base, baseb);
-        else if (mode == 2) hipLaunchKernelGGL(bench<2>, dim3(nwg), dim3(256), ldsb, 0, d_t, d_sink, rows, base, baseb);
-        else hipLaunchKernelGGL(bench<3>, dim3(nwg), dim3(256), ldsb, 0, d_t, d_sink, rows, base, baseb);
+        if (mode == 0) hipLaunchKernelGGL(bench<0>, dim3(nwg), dim3(256), ldsb, 0, d_t, d_sink, rows, base, baseb, basec);
+        else if (mode == 1) hipLaunchKernelGGL(bench<1>, dim3(nwg), dim3(256), ldsb, 0, d_t, d_sink, rows, base, baseb, basec);
+        else if (mode == 2) hipLaunchKernelGGL(bench<2>, dim3(nwg), dim3(256), ldsb, 0, d_t, d_sink, rows, base, baseb, basec);
+        else if (mode == 3) hipLaunchKernelGGL(bench<3>, dim3(nwg), dim3(256), ldsb, 0, d_t, d_sink, rows, base, baseb, basec);
+        else hipLaunchKernelGGL(bench<4>, dim3(nwg), dim3(256), ldsb, 0, d_t, d_sink, rows, base, baseb, basec);
     };
     go();
     hipDeviceSynchronize();
@@ -334,7 +372,7 @@ int main(int argc, char **argv) {
     ms /= it;
     const double products = (double)nwg * 4 * rows * (mode == 3 ? 4 : 8);  // per-wave outputs
     printf("mode=%s nwg=%d lds=%d rows=%d: %.4f ms, %.2f G wave-products/s, %.1f ns per wave-product per CU\n",
-           mode == 0 ? "call" : mode == 1 ? "inline" : mode == 2 ? "index" : "call4", nwg, ldsb, rows, ms, products / ms / 1e6, ms * 1e6 * 256 / products);
+           mode == 0 ? "call" : mode == 1 ? "inline" : mode == 2 ? "index" : mode == 3 ? "call4" : "chain1", nwg, ldsb, rows, ms, products / ms / 1e6, ms * 1e6 * 256 / products);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) printf("error %s\n", hipGetErrorString(err));
     return 0;
