@@ -48,6 +48,9 @@ def parse():
     p.add_argument("--root-steps", type=int, default=3,
                    help="N>1: steps of the root-resident variant (RCCL scatter -> encode -> gather); 0 = skip")
     p.add_argument("--no-sweep", action="store_true", help="skip the C2/C3/C4/Tester-shape leg")
+    p.add_argument("--backend", default="nccl",
+                   help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse the "
+                        "multi-rank path with several ranks on one GPU)")
     p.add_argument("--dry-run", action="store_true",
                    help="launcher check without a GPU: ranks join a gloo group and rank 0 reports them")
     return p.parse_args()
@@ -387,14 +390,19 @@ def main():
     import torch
     import torch.distributed as dist
 
+    # rank r on GPU r; with fewer GPUs than ranks (a gloo rehearsal on one GPU) ranks share them
+    dev = local % max(1, torch.cuda.device_count())
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(args.backend)
         world = dist.get_world_size()
     else:
         torch.cuda.set_device(0)
     import shorthair_amd as sh
-    assert sh.lib.cauchy_256_batch_init(local if world > 1 else 0) == 0
+    assert sh.lib.cauchy_256_batch_init(dev) == 0
 
     k, m, B, G = args.k, args.m, args.block, args.groups
     emax = min(k, m)

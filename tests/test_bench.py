@@ -61,3 +61,20 @@ def test_cpu_baseline_native_modes():
     assert set(cpu["modes"]) == {"shipped_t1", "init_t1", "shipped_t2", "init_t2"}
     assert cpu["value"] == max(cpu["modes"]["shipped_t2"]["GiBps"], cpu["modes"]["init_t2"]["GiBps"])
     assert cpu["cpu"]
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_on_one_gpu():
+    """The whole N > 1 path of `bench.py --gpus 2` (spawn, process group, per-rank shards,
+    barrier + max-over-ranks timing, root-resident scatter/encode/gather) with both ranks on the
+    box's one GPU over gloo: the JSON line reports 2 GPUs and the root shards round-trip."""
+    import json
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                        "--steps", "2", "--warmup", "1", "--groups", "256", "--root-steps", "1", "--no-cpu",
+                        "--host-calls", "0", "--no-sweep"], capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["value"] > 0 and line["config"]["parallelism"] == "groups sharded x2"
+    assert line["root_resident"].get("root_shard_roundtrip_ok") is True
