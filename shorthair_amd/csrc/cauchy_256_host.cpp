@@ -254,6 +254,7 @@ int encode_batch(int k, int m, int B, int groups, const uint8_t *d_in, uint8_t *
 // Workspace carve for decode of `groups` groups.
 struct DecodeWS {
     bool fixed;       // stage A by a compile-time-scheduled kernel, stage B by stageb_fixed
+    bool small;       // ... and stage B by stageb_small (nq <= 16 word columns: byte coefficients)
     int emax, ldA, ldB, nres;  // nres: residual rows per group (m when fixed, else emax)
     int *e;
     uint8_t *rec_idx, *erasures, *coefA, *coefB, *residual, *recovered, *pos, *rpos, *rrow;
@@ -265,6 +266,7 @@ size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool n
     const sh::Geometry geo = sh::fixed_geometry(B);
     w.emax = std::min(k, m);
     w.fixed = sh::has_fixed(k, m, B) && sh::stageb_fixed_ok(geo, w.emax);
+    w.small = w.fixed && sh::stageb_small_ok(geo, w.emax);
     w.ldA = w.fixed ? 0 : round4(k);
     w.ldB = (w.emax + 7) & ~7;  // stage-B coefficients [i][ldB] (transposed, 8-entry rows)
     w.nres = w.fixed ? m : w.emax;
@@ -281,8 +283,9 @@ size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool n
     w.rec_idx = take(G * w.emax);
     w.erasures = take(G * w.emax);
     w.coefA = w.fixed ? nullptr : take(G * w.coefA_gs);
-    w.coefB = w.fixed ? nullptr : take(G * w.coefB_gs);
-    w.targets = w.fixed ? reinterpret_cast<uint64_t *>(take(G * w.emax * w.ldB * sizeof(uint64_t))) : nullptr;
+    w.coefB = (w.fixed && !w.small) ? nullptr : take(G * w.coefB_gs);
+    w.targets = (w.fixed && !w.small) ? reinterpret_cast<uint64_t *>(take(G * w.emax * w.ldB * sizeof(uint64_t)))
+                                      : nullptr;
     w.rrow = w.fixed ? take(G * round4(w.emax)) : nullptr;
     w.pos = w.fixed ? take(G * round4(k)) : nullptr;
     w.rpos = w.fixed ? take(G * round4(m)) : nullptr;
@@ -292,6 +295,23 @@ size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool n
 }
 
 hipError_t launch_stage_b(const DecodeWS &w, int n_in, int B, int groups, uint8_t *dst, hipStream_t s) {
+    if (w.small) {
+        sh::StageBSmallArgs f{};
+        f.in = w.residual;
+        f.in_gstride = static_cast<long long>(n_in) * B;
+        f.out = dst;
+        f.out_gstride = static_cast<long long>(w.emax) * B;
+        f.e = w.e;
+        f.rrow = w.rrow;
+        f.ldR = round4(w.emax);
+        f.coefT = w.coefB;
+        f.coefT_gstride = w.coefB_gs;
+        f.ldT = w.ldB;
+        f.emax = w.emax;
+        f.groups = groups;
+        f.geo = sh::fixed_geometry(B);
+        return sh::launch_stageb_small(f, s);
+    }
     if (w.fixed) {
         sh::StageBFixedArgs f{};
         f.in = w.residual;

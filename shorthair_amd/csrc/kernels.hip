@@ -354,15 +354,19 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
     // copy-and-XOR snippet kernel, zero elsewhere. Fixed path: the address of the accumulating
     // snippet of each coefficient (the null snippet for zeros and for outputs j >= e), plus the
     // residual row of each received recovery block.
-    uint8_t *Bc = fixed_mode ? nullptr : a.coefB + static_cast<long long>(g) * a.coefB_gstride;
+    // Byte coefficients (generic path, and the small-block stage B after a compile-time stage A:
+    // targets == nullptr) or snippet addresses (stageb_fixed).
+    uint8_t *Bc = a.targets ? nullptr : a.coefB + static_cast<long long>(g) * a.coefB_gstride;
     // fixed layout [g][j / 8][i][j % 8]: one wave's 8 addresses of consecutive rows are contiguous
-    uint64_t *Tg = fixed_mode ? a.targets + static_cast<long long>(g) * emax * a.ldB : nullptr;
+    uint64_t *Tg = a.targets ? a.targets + static_cast<long long>(g) * emax * a.ldB : nullptr;
     const uint64_t tnull = a.snip_base + static_cast<uint64_t>(SNIP_NULL) * SNIP_STRIDE;
     if (fixed_mode) {
-        // every address stage B reads is written exactly once: (i < e, j < e) by put() below,
-        // the unused outputs j in [e, ldB) here
         uint8_t *rr = a.rrow + static_cast<long long>(g) * a.ldR;
         for (int i = lane; i < e; i += 64) rr[i] = s_rrow[i];
+    }
+    if (Tg) {
+        // every address stage B reads is written exactly once: (i < e, j < e) by put() below,
+        // the unused outputs j in [e, ldB) here
         const int pad = a.ldB - e;
         for (int t = lane; t < e * pad; t += 64) {
             const int i = t / pad, j = e + (t - i * pad);
@@ -372,7 +376,7 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
         for (int t = lane; t < emax * a.ldB; t += 64) Bc[t] = 0;
     }
     auto put = [&](int j, int i, uint32_t v) {
-        if (fixed_mode)
+        if (Tg)
             Tg[(static_cast<long long>(j >> 3) * emax + i) * 8 + (j & 7)] =
                 v ? a.snip_base + static_cast<uint64_t>(v) * SNIP_STRIDE : tnull;
         else

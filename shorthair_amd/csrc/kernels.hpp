@@ -133,6 +133,25 @@ struct StageBFixedArgs {
 };
 bool stageb_fixed_ok(const Geometry &geo, int emax);
 hipError_t launch_stageb_fixed(const StageBFixedArgs &a, hipStream_t stream);
+// Decode stage B for small blocks after a compile-time stage A (csrc/stageb.hip, stageb_small):
+// per-lane coefficients, so one wave serves 64 / nq groups.
+struct StageBSmallArgs {
+    const uint8_t *in;        // [G][in_gstride] residual rows (all m generator rows)
+    long long in_gstride;
+    uint8_t *out;             // [G][out_gstride]
+    long long out_gstride;
+    const int *e;             // [G] received recovery blocks = outputs (<= 0: nothing to do)
+    const uint8_t *rrow;      // [G][ldR] residual row of the i-th received recovery block
+    int ldR;
+    const uint8_t *coefT;     // [G][emax][ldT]: entry [i][j] = S^-1[j][i] (0 past e)
+    long long coefT_gstride;
+    int ldT;                  // multiple of 8
+    int emax;
+    int groups;
+    Geometry geo;
+};
+bool stageb_small_ok(const Geometry &geo, int emax);
+hipError_t launch_stageb_small(const StageBSmallArgs &a, hipStream_t stream);
 // Address of stage-B snippet 0 in the loaded code object (one tiny kernel launch + copy).
 hipError_t stageb_snip_base(uint64_t *out_host, hipStream_t stream);
 constexpr int SNIP_STRIDE = 72;   // bytes per stage-B snippet (gen_fixed_kernels.py)

@@ -27,6 +27,7 @@ namespace sh {
 
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t ldw_b(const uint8_t *p) {
     uint32_t w;
@@ -334,6 +335,127 @@ __global__ __launch_bounds__(256, 4) void stageb_fixed(StageBFixedArgs a) {
 #pragma unroll
         for (int b = 0; b < 8; ++b) __builtin_memcpy(row + b * geo.sub, &acc[j][b], 4);
     }
+}
+
+// Decode stage B for small blocks (fixed geometry with nq <= 16 word columns, B <= 512). A
+// group fills only nq lanes there, and a snippet's coefficient is wave-uniform, so stageb_fixed
+// would leave 64 - nq lanes idle; here each lane applies its own group's coefficients instead and
+// one wave serves 64 / nq groups. Per residual row every lane writes its 30 window-table entries
+// (the reference's win_encode tables, cauchy_256.cpp:1426-1445, of its column's 8 words) to LDS
+// laid out [entry][lane]; coefficient c is applied as 8 x (two table lookups + one XOR3) with the
+// 16 entry indices of c (lo and 16 + hi of c * 2^b) read from a 256 x 16-byte table, each lookup
+// address one v_perm_b32 (entry into byte 1, lane * 4 into byte 0) and one ds_read_b32. One wave
+// per workgroup, so the table base is a compile-time offset.
+bool stageb_small_ok(const Geometry &geo, int emax) {
+    return geo.nq % 4 == 0 && geo.nq <= 16 && geo.sub >= 16 && emax >= 1 && emax <= 128;
+}
+
+__global__ __launch_bounds__(64) void stageb_small(StageBSmallArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t tab[32 * 64];  // 8 KB window tables [entry][lane]
+    __shared__ __attribute__((aligned(16))) uint32_t rbt[256 * 4];  // entry bytes of c * 2^b, b = 0..7
+    __shared__ uint8_t rrs[16][128];                                // row lists of the wave's groups
+    const Geometry geo = a.geo;
+    const int lane = threadIdx.x;
+    const int gpw = 64 / geo.nq;
+    const int gs = lane / geo.nq, q = lane - gs * geo.nq;
+    const int g0 = blockIdx.x * gpw;
+    const bool valid = gs < gpw && g0 + gs < a.groups;
+    const int g = valid ? g0 + gs : g0;
+    const int j0 = blockIdx.y * 8;
+    for (int c = lane; c < 256; c += 64) {
+        uint32_t w[4] = {0, 0, 0, 0};
+        uint32_t v = static_cast<uint32_t>(c);
+        for (int b = 0; b < 8; ++b) {
+            w[b >> 1] |= ((v & 15u) | ((16u + (v >> 4)) << 8)) << (16 * (b & 1));
+            v = (v << 1) ^ ((v & 0x80u) ? 0x187u : 0u);  // c * 2^b in GF(256)/0x187
+        }
+        for (int t = 0; t < 4; ++t) rbt[c * 4 + t] = w[t];
+    }
+    tab[lane] = 0;            // T0[0]
+    tab[16 * 64 + lane] = 0;  // T1[0]
+    for (int t = lane; t < gpw * a.emax; t += 64) {
+        const int sl = t / a.emax, i = t - sl * a.emax;
+        const int gg = g0 + sl;
+        rrs[sl][i] = (gg < a.groups && i < a.e[gg]) ? a.rrow[static_cast<long long>(gg) * a.ldR + i] : 0;
+    }
+    __syncthreads();
+    const int el = valid ? max(a.e[g], 0) : 0;
+    int emx = el;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) emx = max(emx, __shfl_xor(emx, o));
+    emx = __builtin_amdgcn_readfirstlane(emx);
+    if (emx <= j0) return;  // no lane has an output in this chunk
+
+    const uint8_t *res = a.in + static_cast<long long>(g) * a.in_gstride + colx_off(q, geo.nq, geo.sub);
+    const uint8_t *cp = a.coefT + static_cast<long long>(g) * a.coefT_gstride + j0;
+    const uint32_t lane4 = static_cast<uint32_t>(lane) * 4u;
+    auto load = [&](int i, uint32_t (&d)[8], uint64_t &cc) {
+        const int r = rrs[gs][min(i, max(el - 1, 0))];
+        const uint8_t *p = res + static_cast<long long>(r) * geo.B;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) __builtin_memcpy(&d[s], p + s * geo.sub, 4);
+        cc = 0;
+        if (i < el) __builtin_memcpy(&cc, cp + static_cast<long long>(i) * a.ldT, 8);
+    };
+    auto lk = [&](uint32_t addr) { return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(tab) + addr); };
+
+    uint32_t acc[8][8];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[jj][b] = 0;
+    uint32_t d[8], dn[8];
+    uint64_t cc, ccn;
+    load(0, d, cc);
+    for (int i = 0; i < emx; ++i) {
+        if (i + 1 < emx) load(i + 1, dn, ccn);  // next row in flight under this row's work
+        // window tables of this row's words: T0 from d0..d3, T1 from d4..d7
+        const uint32_t e3 = d[0] ^ d[1], e5 = d[0] ^ d[2], e6 = d[1] ^ d[2], e9 = d[0] ^ d[3];
+        const uint32_t e10 = d[1] ^ d[3], e12 = d[2] ^ d[3], e7 = e3 ^ d[2];
+        const uint32_t f3 = d[4] ^ d[5], f5 = d[4] ^ d[6], f6 = d[5] ^ d[6], f9 = d[4] ^ d[7];
+        const uint32_t f10 = d[5] ^ d[7], f12 = d[6] ^ d[7], f7 = f3 ^ d[6];
+        const uint32_t tv[32] = {0, d[0], d[1], e3, d[2], e5, e6, e7, d[3], e9, e10, e3 ^ d[3], e12, e5 ^ d[3], e6 ^ d[3], e7 ^ d[3],
+                                 0, d[4], d[5], f3, d[6], f5, f6, f7, d[7], f9, f10, f3 ^ d[7], f12, f5 ^ d[7], f6 ^ d[7], f7 ^ d[7]};
+#pragma unroll
+        for (int t = 1; t < 32; ++t)
+            if (t != 16) tab[t * 64 + lane] = tv[t];
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+            const uint32_t c = static_cast<uint32_t>(cc >> (8 * jj)) & 0xFFu;
+            const u32x4 rb = *reinterpret_cast<const u32x4 *>(&rbt[c * 4]);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const uint32_t w = rb[b >> 1];
+                const uint32_t k = 2u * (b & 1);  // byte k: T0 entry, byte k + 1: T1 entry
+                const uint32_t a0 = __builtin_amdgcn_perm(w, lane4, 0x0C0C0000u | ((4u + k) << 8));
+                const uint32_t a1 = __builtin_amdgcn_perm(w, lane4, 0x0C0C0000u | ((5u + k) << 8));
+                acc[jj][b] = __builtin_amdgcn_bitop3_b32(acc[jj][b], lk(a0), lk(a1), 0x96);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int s = 0; s < 8; ++s) d[s] = dn[s];
+        cc = ccn;
+    }
+    if (!valid) return;
+    uint8_t *out = a.out + static_cast<long long>(g) * a.out_gstride + colx_off(q, geo.nq, geo.sub);
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+        if (j0 + jj >= el) break;
+        uint8_t *row = out + static_cast<long long>(j0 + jj) * geo.B;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) __builtin_memcpy(row + b * geo.sub, &acc[jj][b], 4);
+    }
+}
+
+hipError_t launch_stageb_small(const StageBSmallArgs &a, hipStream_t stream) {
+    if (a.groups <= 0 || a.emax <= 0) return hipSuccess;
+    if (!stageb_small_ok(a.geo, a.emax)) return hipErrorNotSupported;
+    const int gpw = 64 / a.geo.nq;
+    dim3 grid(static_cast<unsigned>((a.groups + gpw - 1) / gpw), (a.emax + 7) / 8, 1);
+    hipLaunchKernelGGL(stageb_small, grid, dim3(64), 0, stream, a);
+    return hipGetLastError();
 }
 
 bool stageb_fixed_ok(const Geometry &geo, int emax) {

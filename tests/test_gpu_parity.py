@@ -176,7 +176,12 @@ def _decode_inputs(k, m, B, G, cfg, e_fixed):
 @pytest.mark.parametrize("k,m,B,G,e_fixed", [(200, 32, 1400, 8192, 0), (200, 32, 1400, 2048, 32),
                                              (64, 16, 1400, 1024, 0), (28, 4, 256, 700, 0),
                                              (112, 16, 65536, 6, 0), (128, 128, 8, 64, 0),
-                                             (30, 9, 48, 500, 9)])
+                                             (30, 9, 48, 500, 9),
+                                             # small blocks on the compile-time path (stageb_small,
+                                             # nq = 4 / 8 / 12 / 16 word columns, shifted chunks)
+                                             (28, 4, 128, 3001, 0), (224, 32, 256, 601, 0),
+                                             (112, 16, 384, 333, 16), (200, 32, 136, 257, 0),
+                                             (200, 56, 512, 129, 0), (64, 16, 264, 77, 0)])
 def test_decode_batch_roundtrip_and_oracle(sh, k, m, B, G, e_fixed):
     """BASELINE configs[2] (8192 x k=200 m=32 1400B, random erasures up to 32): every group's
     recovered blocks equal the erased originals (encode -> erase -> decode round trip, whole
