@@ -243,30 +243,29 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
     __shared__ uint8_t s_exp[512];
     __shared__ uint8_t s_log[256];
     __shared__ uint8_t s_rows[256];
-    __shared__ int s_present[256];      // occurrences of each row value
+    __shared__ uint32_t s_present[64];  // occurrences of each row value, 4 x 8-bit counts per word
     __shared__ uint8_t s_rec[256];      // array index of the i-th recovery block
     __shared__ uint8_t s_rrow[256];     // its generator row r_i = row - k
     __shared__ uint8_t s_era[256];      // j-th erased original row E_j
     __shared__ uint8_t s_x[256], s_y[256];
-    __shared__ int s_la[256], s_lb[256], s_lx[256];
+    __shared__ uint8_t s_la[256], s_lb[256], s_lx[256];  // logs mod 255 (~3.4 KB in all: 32 waves/CU)
     __shared__ uint8_t s_gj[6 * 12];    // [S | I] for the m <= 6 Gauss-Jordan
     __shared__ int s_piv;
 
     for (int i = lane; i < 512; i += 64) s_exp[i] = a.gf_exp[i];
-    for (int i = lane; i < 256; i += 64) {
-        s_log[i] = static_cast<uint8_t>(a.gf_log[i]);
-        s_present[i] = 0;
-    }
+    for (int i = lane; i < 256; i += 64) s_log[i] = static_cast<uint8_t>(a.gf_log[i]);
+    s_present[lane] = 0;
+    auto present = [&](int r) { return static_cast<int>((s_present[r >> 2] >> (8 * (r & 3))) & 0xFFu); };
     const uint8_t *rows = a.rows + static_cast<long long>(g) * a.rows_gstride;
     for (int j = lane; j < k; j += 64) s_rows[j] = rows[j];
     __syncthreads();
-    for (int j = lane; j < k; j += 64)
-        atomicAdd(&s_present[s_rows[j]], 1);
+    for (int j = lane; j < k; j += 64)  // a row occurs at most k <= 255 times: no carry between counts
+        atomicAdd(&s_present[s_rows[j] >> 2], 1u << (8 * (s_rows[j] & 3)));
     __syncthreads();
     // A row listed twice, or a recovery row past the generator (row >= k + m), is outside the
     // reference's contract (it would decode garbage): the group is left untouched and reported.
     bool bad = false;
-    for (int r = lane; r < 256; r += 64) bad |= s_present[r] > 1 || (r >= k + m && s_present[r] > 0);
+    for (int r = lane; r < 256; r += 64) bad |= present(r) > 1 || (r >= k + m && present(r) > 0);
     if (__ballot(bad) != 0ull) {
         if (lane == 0) {
             a.e_out[g] = -1;
@@ -291,7 +290,7 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
     int nera = 0;
     for (int base = 0; base < k; base += 64) {
         const int x = base + lane;
-        const bool miss = (x < k) && !s_present[x];
+        const bool miss = (x < k) && !present(x);
         const unsigned long long mask = __ballot(miss);
         if (miss) {
             const int pos = nera + __popcll(mask & ((1ull << lane) - 1ull));
@@ -364,17 +363,19 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
         uint8_t *rr = a.rrow + static_cast<long long>(g) * a.ldR;
         for (int i = lane; i < e; i += 64) rr[i] = s_rrow[i];
     }
-    if (Tg) {
-        // every address stage B reads is written exactly once: (i < e, j < e) by put() below,
-        // the unused outputs j in [e, ldB) here
-        const int pad = a.ldB - e;
-        for (int t = lane; t < e * pad; t += 64) {
-            const int i = t / pad, j = e + (t - i * pad);
-            Tg[(static_cast<long long>(j >> 3) * emax + i) * 8 + (j & 7)] = tnull;
+    // Every entry stage B reads is written exactly once: the coefficient of (i < e, j < e), the
+    // null snippet / zero for the unused outputs j in [e, ldB), and zero rows i >= e (bytes only).
+    auto fill_unused = [&]() {
+        if (Tg) {
+            const int pad = a.ldB - e;
+            for (int t = lane; t < e * pad; t += 64) {
+                const int i = t / pad, j = e + (t - i * pad);
+                Tg[(static_cast<long long>(j >> 3) * emax + i) * 8 + (j & 7)] = tnull;
+            }
+        } else {
+            for (int t = lane; t < emax * a.ldB; t += 64) Bc[t] = 0;
         }
-    } else {
-        for (int t = lane; t < emax * a.ldB; t += 64) Bc[t] = 0;
-    }
+    };
     auto put = [&](int j, int i, uint32_t v) {
         if (Tg)
             Tg[(static_cast<long long>(j >> 3) * emax + i) * 8 + (j & 7)] =
@@ -399,19 +400,33 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
                     lb -= s_log[yt ^ s_y[q]];
                 }
             }
-            s_la[t] = la;
-            s_lb[t] = lb;
+            s_la[t] = static_cast<uint8_t>(mod255(la));
+            s_lb[t] = static_cast<uint8_t>(mod255(lb));
             s_lx[t] = s_log[xt];
         }
         __syncthreads();
-        // (writes after the zero fill above: same wave, program order)
-        for (int t = lane; t < e * e; t += 64) {
-            const int j = t / e, i = t - j * e;
-            const int l = s_la[j] + s_lb[i] - s_lx[j] - s_log[s_x[j] ^ s_y[i]];
-            put(j, i, s_exp[mod255(l)]);
+        auto coef = [&](int j, int i) -> uint32_t {
+            return s_exp[mod255(s_la[j] + s_lb[i] - s_lx[j] - s_log[s_x[j] ^ s_y[i]])];
+        };
+        // Walk the output in memory order so every store instruction writes contiguous bytes,
+        // the unused entries included: addresses [j/8][i][j%8] (i < e), bytes [i][j] (i < emax).
+        if (Tg) {
+            const int nt = (a.ldB >> 3) * e * 8;
+            for (int t = lane; t < nt; t += 64) {
+                const int jb = t / (e * 8), r = t - jb * e * 8, i = r >> 3, j = jb * 8 + (r & 7);
+                const uint32_t c = j < e ? coef(j, i) : 0u;
+                Tg[(static_cast<long long>(jb) * emax + i) * 8 + (r & 7)] =
+                    c ? a.snip_base + static_cast<uint64_t>(c) * SNIP_STRIDE : tnull;
+            }
+        } else {
+            for (int t = lane; t < emax * a.ldB; t += 64) {
+                const int i = t / a.ldB, j = t - i * a.ldB;
+                Bc[t] = static_cast<uint8_t>(i < e && j < e ? coef(j, i) : 0u);
+            }
         }
         return;
     }
+    fill_unused();  // the Gauss-Jordan below writes the (i < e, j < e) entries with put()
     // m <= 6: Gauss-Jordan on [S | I] (e <= 5).
     const int w = 2 * e;
     for (int t = lane; t < e * w; t += 64) {
