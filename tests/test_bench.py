@@ -28,7 +28,7 @@ def test_traffic_lookup_requires_matching_build():
     assert (t is None) == (src is None)
     if t is not None:  # a summary of this very build: per-kernel read/write/total bytes
         for v in t.values():
-            assert v["hbm_bytes"] == v["read_bytes"] + v["write_bytes"] > 0
+            assert v["hbm_bytes"] > 0 and abs(v["hbm_bytes"] - v["read_bytes"] - v["write_bytes"]) <= 1  # rounding
 
 
 @pytest.mark.parametrize("n", [1, 2, 3])
