@@ -377,14 +377,13 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
     sa.snip_base = c.snip_base;
     sa.errors = c.d_errors;
     hipEvent_t *ev = nullptr;
-    {
+    {  // check and claim the slot in one critical section (profile() may resize the ring)
         std::lock_guard<std::mutex> g(c.mu);
-        if (!c.evq.empty()) ev = c.evq[c.ev_next].data();
-    }
-    if (ev) {
-        std::lock_guard<std::mutex> g(c.mu);
-        c.ev_next = (c.ev_next + 1) % static_cast<int>(c.evq.size());
-        c.ev_count = std::min(c.ev_count + 1, static_cast<int>(c.evq.size()));
+        if (!c.evq.empty()) {
+            ev = c.evq[c.ev_next].data();
+            c.ev_next = (c.ev_next + 1) % static_cast<int>(c.evq.size());
+            c.ev_count = std::min(c.ev_count + 1, static_cast<int>(c.evq.size()));
+        }
     }
     if (ev) SH_CHECK(hipEventRecord(ev[0], s));
     SH_CHECK(sh::launch_decode_setup(sa, groups, s));
