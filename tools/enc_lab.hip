@@ -1,0 +1,294 @@
+// Measurement lab for the compile-time encode kernel (never part of the product): times the
+// product kernel structure against experimental launch structures built from the SAME generated
+// body, and records per-workgroup timestamps.
+//
+//   tools/enc_lab.sh  (generates the bodies, builds, runs; see there)
+//
+// Variants (all encode k=200 m=32 B=1400, 8192 groups unless --groups):
+//   base   the product kernel (scratch aliases the ring), one tile per workgroup
+//   sep    one tile per workgroup, store scratch in its own LDS (control for `pers`)
+//   pers   persistent workgroups (2 per CU), tile v = xcd_tile(blockIdx + i * grid): the next
+//          tile's first ring DMAs are issued right after the last compute step, before the
+//          current tile's epilogue stores (scratch separate from the ring)
+// Stamps (s_memrealtime, 100 MHz) per tile: start, first ring wait passed, last step done, end,
+// plus the XCC / CU of the workgroup -> lab_stamps_<variant>.csv.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <algorithm>
+#include <vector>
+
+#include "fixed_k200_m32.inc"
+
+#define CK(x)                                                                             \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess) {                                                           \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(1);                                                                      \
+        }                                                                                 \
+    } while (0)
+
+namespace lab {
+using namespace sh;
+using namespace sh::fixed;
+
+#ifndef LAB_R
+#define LAB_R 16
+#endif
+using S = Shape<200, 32, 4, 2, LAB_R, true>;
+constexpr int NSTAMP = 64;  // start, first, last, end, hwid, -, then one per ring wait (after its barrier)
+
+__device__ __forceinline__ uint64_t now() { return __builtin_amdgcn_s_memrealtime(); }
+
+template <bool ON>
+struct Stamp {
+    uint64_t *p;  // this tile's record
+    __device__ __forceinline__ void put(int i) const {
+        if (ON && threadIdx.x == 0) p[i] = now();
+    }
+};
+
+// Product Src plus hooks: stamps, and (persistent) skipping the DMAs already issued for this
+// tile by the previous tile's epilogue / issuing the next tile's.
+template <bool PERS, bool ST, bool ALN = false>
+struct LabSrc : Src<S, false> {
+    using Base = Src<S, false>;
+    Stamp<ST> st;
+    bool prefetched;          // this tile's first R-1 DMAs were issued by the previous tile
+    bool has_next;            // persistent: nx is the tile after this one
+    Base nx;
+
+    __device__ __forceinline__ void issue(int x, const typename Base::Pre &pr) const {
+        if (PERS && prefetched && x < S::R - 1) return;
+        Base::issue(x, pr);
+    }
+    template <int T, int I>
+    __device__ __forceinline__ void wait() const {
+        Base::template wait<T, I>();
+        if (T == 3) st.put(1);  // the first wait of the schedule (S = 4)
+        st.put(6 + T / 4);
+    }
+    __device__ __forceinline__ void release() const {
+        st.put(2);
+        Base::release();  // every wave is past its last ring read
+        if (PERS && has_next) {
+            typename Base::Pre pr;
+#pragma unroll
+            for (int t = 0; t < S::R - 1; ++t) nx.issue(t, pr);
+        }
+    }
+};
+
+__device__ __forceinline__ int prologue(const FixedArgs &a, uint8_t *lds, uint8_t *scratch, Src<S, false> &src,
+                                        Sink &sink, long long col0) {
+    WGInfo w;
+    w.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    w.lane = threadIdx.x & 63;
+    const int part = w.wave % S::P;
+    const int cw = w.wave / S::P;
+    w.c = cw * 64 + w.lane;
+    w.col0 = col0;
+    w.lo = 0;
+    w.hi = static_cast<long long>(a.groups) * a.geo.nq;
+    const int nq = a.geo.nq;
+    w.g_first = static_cast<int>((col0 > 0 ? col0 : 0) / nq);
+    const long long col = w.col0 + w.c;
+    w.valid = col >= w.lo && col < w.hi;
+    const int g = w.valid ? static_cast<int>(col / nq) : w.g_first;
+    w.q = static_cast<int>(col - static_cast<long long>(g) * nq);
+    w.gl = g - w.g_first;
+    src.init(a, w, lds, lds);
+    sink.init(a, w, scratch + w.wave * 2048);
+    return part;
+}
+
+__device__ __forceinline__ uint32_t hwid() {
+    const uint32_t hw = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));    // HW_REG_HW_ID
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11));  // HW_REG_XCC_ID
+    return (xcc & 0xF) << 16 | (hw >> 8 & 0xFFFF);
+}
+
+// Timing-only (wrong results): every DMA source rounded down to 16 bytes.
+template <class L>
+__device__ __forceinline__ void align_src(L &src) {
+#pragma unroll
+    for (int j = 0; j < S::DPW; ++j)
+        if (src.dbase[j] != OOR) src.dbase[j] &= ~15u;
+}
+
+// MODE 0: base (scratch aliases ring); 1: sep; 2: pers; 3: base with 16-byte-aligned DMA sources
+template <int MODE, bool ST>
+__global__ __launch_bounds__(S::NT, 4) void kern(FixedArgs a, uint64_t *stamps, int ntiles) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t *scratch = (MODE == 0 || MODE == 3) ? lds : lds + S::R * S::SLOT;
+    if (MODE != 2) {
+        const int tile = xcd_tile(blockIdx.x, gridDim.x);
+        LabSrc<false, ST> src;
+        src.st.p = stamps + static_cast<size_t>(tile) * NSTAMP;
+        src.st.put(0);
+        src.prefetched = false;
+        src.has_next = false;
+        Sink sink;
+        const int part = prologue(a, lds, scratch, src, sink, static_cast<long long>(tile) * S::COLS);
+        if (MODE == 3) align_src(src);
+        run_k200_m32_enc(part, src, sink);
+        src.st.put(3);
+        if (ST && threadIdx.x == 0) stamps[static_cast<size_t>(tile) * NSTAMP + 4] = hwid() | (uint64_t)blockIdx.x << 32;
+        return;
+    }
+    LabSrc<true, ST> cur;
+    Sink sink, nsink;
+    int v = blockIdx.x;
+    if (v >= ntiles) return;
+    int tile = xcd_tile(v, ntiles);
+    int part = prologue(a, lds, scratch, cur, sink, static_cast<long long>(tile) * S::COLS);
+    cur.prefetched = false;
+    for (;;) {
+        cur.st.p = stamps + static_cast<size_t>(tile) * NSTAMP;
+        cur.st.put(0);
+        const int vn = v + gridDim.x;
+        const int tn = vn < ntiles ? xcd_tile(vn, ntiles) : -1;
+        cur.has_next = tn >= 0;
+        if (tn >= 0) prologue(a, lds, scratch, cur.nx, nsink, static_cast<long long>(tn) * S::COLS);
+        run_k200_m32_enc(part, cur, sink);
+        cur.st.put(3);
+        if (ST && threadIdx.x == 0) stamps[static_cast<size_t>(tile) * NSTAMP + 4] = hwid() | (uint64_t)blockIdx.x << 32;
+        if (tn < 0) break;
+        static_cast<Src<S, false> &>(cur) = cur.nx;
+        cur.prefetched = true;
+        sink = nsink;
+        v = vn;
+        tile = tn;
+    }
+}
+
+__global__ void fill(uint32_t *p, size_t n, uint32_t seed) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        uint32_t x = static_cast<uint32_t>(i) * 0x9E3779B9u ^ seed;
+        x ^= x >> 16; x *= 0x85EBCA6Bu; x ^= x >> 13; x *= 0xC2B2AE35u; x ^= x >> 16;
+        p[i] = x;
+    }
+}
+
+__global__ void diff(const uint32_t *a, const uint32_t *b, size_t n, unsigned long long *cnt) {
+    unsigned long long c = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        c += a[i] != b[i];
+    if (c) atomicAdd(cnt, c);
+}
+}  // namespace lab
+
+int main(int argc, char **argv) {
+    using namespace lab;
+    int groups = 8192, iters = 30;
+    const char *only = nullptr;
+    for (int i = 1; i < argc; ++i) {
+        if (!strcmp(argv[i], "--groups")) groups = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--iters")) iters = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--only")) only = argv[++i];
+    }
+    const int k = 200, m = 32, B = 1400;
+    FixedArgs a{};
+    a.geo = make_geometry(B);
+    a.geo = fixed_geometry(B);
+    a.groups = groups;
+    a.in_gstride = (long long)k * B;
+    a.in_bytes = a.in_gstride * groups;
+    a.out_gstride = (long long)m * B;
+    a.out_bytes = a.out_gstride * groups;
+    uint8_t *in, *out, *ref;
+    CK(hipMalloc(&in, a.in_bytes));
+    CK(hipMalloc(&out, a.out_bytes));
+    CK(hipMalloc(&ref, a.out_bytes));
+    hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, (uint32_t *)in, (size_t)a.in_bytes / 4, 0x1234u);
+    a.in = in;
+    a.groups_per_wg = (S::COLS - 1) / a.geo.nq + 2;
+    const long long cols = (long long)groups * a.geo.nq;
+    const int ntiles = (int)((cols + S::COLS - 1) / S::COLS);
+    uint64_t *stamps;
+    CK(hipMalloc(&stamps, (size_t)ntiles * NSTAMP * 8));
+    unsigned long long *cnt;
+    CK(hipMalloc(&cnt, 8));
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    const int cus = prop.multiProcessorCount;
+
+    struct V { const char *name; void (*k)(FixedArgs, uint64_t *, int); void (*ks)(FixedArgs, uint64_t *, int); size_t lds; int grid; };
+    const size_t ring = (size_t)S::R * S::SLOT, scr = (size_t)S::NW * 2048;
+    std::vector<V> vs = {
+        {"base", kern<0, false>, kern<0, true>, ring, ntiles},
+#ifdef LAB_MORE
+        {"sep", kern<1, false>, nullptr, ring + scr, ntiles},
+        {"pers", kern<2, false>, kern<2, true>, ring + scr, 2 * cus},
+#endif
+        {"algn", kern<3, false>, kern<3, true>, ring, ntiles},
+    };
+    printf("tiles %d, R %d, lds base %zu sep %zu, CUs %d\n", ntiles, S::R, ring, ring + scr, cus);
+    for (auto &v : vs) {
+        CK(hipFuncSetAttribute((const void *)v.k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)v.lds));
+        if (v.ks) CK(hipFuncSetAttribute((const void *)v.ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)v.lds));
+    }
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    bool have_ref = false;
+    for (auto &v : vs) {
+        if (only && !strstr(only, v.name)) continue;
+        a.out = out;
+        CK(hipMemset(out, 0, a.out_bytes));
+        hipLaunchKernelGGL(v.k, dim3(v.grid), dim3(S::NT), v.lds, 0, a, nullptr, ntiles);
+        CK(hipGetLastError());
+        CK(hipDeviceSynchronize());
+        if (!have_ref) {
+            CK(hipMemcpy(ref, out, a.out_bytes, hipMemcpyDeviceToDevice));
+            have_ref = true;
+        } else {
+            CK(hipMemset(cnt, 0, 8));
+            hipLaunchKernelGGL(diff, dim3(2048), dim3(256), 0, 0, (const uint32_t *)out, (const uint32_t *)ref,
+                               (size_t)a.out_bytes / 4, cnt);
+            unsigned long long c;
+            CK(hipMemcpy(&c, cnt, 8, hipMemcpyDeviceToHost));
+            printf("%-6s mismatching dwords vs first variant: %llu\n", v.name, c);
+        }
+        std::vector<float> ms;
+        for (int it = 0; it < 5; ++it) hipLaunchKernelGGL(v.k, dim3(v.grid), dim3(S::NT), v.lds, 0, a, nullptr, ntiles);
+        for (int it = 0; it < iters; ++it) {
+            CK(hipEventRecord(e0, 0));
+            hipLaunchKernelGGL(v.k, dim3(v.grid), dim3(S::NT), v.lds, 0, a, nullptr, ntiles);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float t;
+            CK(hipEventElapsedTime(&t, e0, e1));
+            ms.push_back(t);
+        }
+        std::sort(ms.begin(), ms.end());
+        const double alg = (double)groups * (k + m) * B;
+        printf("%-6s min %.4f med %.4f ms  (%.0f GB/s at median)\n", v.name, ms[0], ms[ms.size() / 2],
+               alg / ms[ms.size() / 2] / 1e6);
+        if (!v.ks) continue;
+        // stamped run
+        CK(hipMemset(stamps, 0, (size_t)ntiles * NSTAMP * 8));
+        hipLaunchKernelGGL(v.ks, dim3(v.grid), dim3(S::NT), v.lds, 0, a, stamps, ntiles);
+        CK(hipDeviceSynchronize());
+        std::vector<uint64_t> h((size_t)ntiles * NSTAMP);
+        CK(hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost));
+        char fn[256];
+        snprintf(fn, sizeof fn, "gpurun_out/lab_stamps_%s.csv", v.name);
+        FILE *f = fopen(fn, "w");
+        if (f) {
+            fprintf(f, "tile,start,first,last,end,xcc,hwid,block,waits\n");
+            for (int t = 0; t < ntiles; ++t) {
+                const uint64_t *r = &h[(size_t)t * NSTAMP];
+                fprintf(f, "%d,%llu,%llu,%llu,%llu,%u,%u,%u,", t, (unsigned long long)r[0], (unsigned long long)r[1],
+                        (unsigned long long)r[2], (unsigned long long)r[3], (unsigned)(r[4] >> 16 & 0xF),
+                        (unsigned)(r[4] & 0xFFFF), (unsigned)(r[4] >> 32));
+                for (int j = 6; j < NSTAMP; ++j) fprintf(f, "%lld ", r[j] ? (long long)(r[j] - r[0]) : -1ll);
+                fprintf(f, "\n");
+            }
+            fclose(f);
+        }
+    }
+    return 0;
+}
