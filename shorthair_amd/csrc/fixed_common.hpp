@@ -229,72 +229,73 @@ struct Src {
 
 };
 
-// Output, transposed through a per-wave 2 KB LDS scratch so every store is 16 contiguous bytes:
-// a lane holds word q of the 8 sub-blocks of a row; it writes them to scratch[b][lane], then
-// reads back two 16-byte items (sub-block b, 4-column chunk t) and stores each with one
-// buffer_store_dwordx4 -- 2 store instructions per row instead of 8 dword stores. A chunk lies
-// in one group (nq % 4 == 0) and is contiguous in memory (the shifted last chunk included).
-// Item i = lane + 64h (h = 0, 1): b = i / 16, t = i % 16. Chunks past the last group get an
-// out-of-range offset, dropped by the buffer unit.
-struct Sink {
+// Output assembled per row across the part's CW column-waves, so every store instruction writes
+// 64 consecutive 16-byte pieces of the output in MEMORY order (about 1 KB contiguous): the
+// CW waves of a part write their words of row y into a shared LDS row image laid out like a ring
+// slot ([sub-block][tile column]), meet at a workgroup barrier, and each then stores 128 pieces
+// taken from the image in memory order -- group by group over the tile, sub-block by sub-block,
+// 4-column chunk by chunk. A group whose columns all lie in the tile is written as one
+// contiguous m*B span by one workgroup within a few microseconds; only the groups split between
+// two tiles are written as per-sub-block runs. (A per-wave transposition, round 2's store path,
+// stored 8 runs of <= 176 bytes per instruction: the encode kernel was 3 % slower with it.) Row images are double-buffered by row parity: a wave
+// reads row y's image before it joins row y+1's barrier, so row y+2 may overwrite it.
+// Every wave of the workgroup joins one barrier per row of the largest part (pad() for the
+// shorter parts). The images ([2][P][SLOT] bytes) alias the ring (after Src::release()).
+template <class S>
+struct RowSink {
     __amdgpu_buffer_rsrc_t rsrc;
-    uint32_t voff[2];         // per item: chunk base + b * sub (or OOR)
+    uint32_t gdst[2];         // per piece: destination offset without the row term (OOR: none)
+    uint32_t lsrc[2];         // per piece: byte offset inside a row image
+    uint32_t wofs;            // this lane's word in a row image (tile column * 4)
     uint32_t B;
-    uint8_t *scr;             // this wave's scratch [8][64] words
-    int lane;
-    __device__ __forceinline__ void init(const FixedArgs &a, const WGInfo &w, uint8_t *scratch) {
+    uint8_t *img;             // this part's row image, even rows (odd rows: + P * SLOT)
+    static_assert(2 * S::P * S::SLOT <= S::R * S::SLOT, "row images must fit inside the ring");
+
+    __device__ __forceinline__ void init(const FixedArgs &a, const WGInfo &w, int part, uint8_t *lds) {
         const Geometry &geo = a.geo;
         rsrc = wg_rsrc(a.out, a.out_bytes, a.out_gstride, w.g_first);
         B = geo.B;
-        lane = w.lane;
-        scr = scratch;
-        const int t = w.lane & 15;
-        const long long colx = w.col0 + (w.c - w.lane) + 4 * t;  // first column of chunk t
-        const int gx = colx >= 0 ? static_cast<int>(colx / geo.nq) : -1;
-        const int qx = static_cast<int>(colx - static_cast<long long>(gx) * geo.nq);
-        const uint32_t base = static_cast<uint32_t>(gx - w.g_first) * static_cast<uint32_t>(a.out_gstride) +
-                              col_off(qx, geo);
-        const bool ok = colx >= w.lo && colx < w.hi;
-#ifdef SH_GEN_STORE_ALIGNED  // measurement build only (see store_row_dw)
-        const uint32_t sstride = 176, abase = (static_cast<uint32_t>(gx - w.g_first) * static_cast<uint32_t>(a.out_gstride) + 4u * qx) & ~15u;
-#else
-        const uint32_t sstride = static_cast<uint32_t>(geo.sub), abase = base;
-#endif
+        wofs = static_cast<uint32_t>(w.c) * 4u;
+        img = lds + part * S::SLOT;
+        const int nq = geo.nq;
+        const long long cs = w.col0 > w.lo ? w.col0 : w.lo;
+        const long long ce = w.col0 + S::COLS < w.hi ? w.col0 + S::COLS : w.hi;
+        const int cw = w.c >> 6;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const int b = (w.lane >> 4) + 4 * h;
-            voff[h] = ok ? abase + static_cast<uint32_t>(b) * sstride : OOR;
-        }
-        sub = static_cast<uint32_t>(geo.sub);
-        {
-            const long long colc = w.col0 + w.c;
-            const int gc = colc >= 0 ? static_cast<int>(colc / geo.nq) : -1;
-            const int qc = static_cast<int>(colc - static_cast<long long>(gc) * geo.nq);
-            dw_off = (colc >= w.lo && colc < w.hi)
-                         ? static_cast<uint32_t>(gc - w.g_first) * static_cast<uint32_t>(a.out_gstride) + col_off(qc, geo)
-                         : OOR;
+            int rem = (cw * 2 + h) * 64 + w.lane;  // piece index in memory order
+            gdst[h] = OOR;
+            lsrc[h] = 0;
+            for (long long g = cs / nq; g * nq < ce; ++g) {  // groups overlapping the tile
+                const int qa = static_cast<int>((cs > g * nq ? cs : g * nq) - g * nq);
+                const int qb = static_cast<int>((ce < (g + 1) * nq ? ce : (g + 1) * nq) - g * nq);
+                const int nch = (qb - qa) >> 2;  // whole chunks: tile and group edges are multiples of 4
+                if (rem < 8 * nch) {
+                    const int b = rem / nch, q = qa + 4 * (rem - b * nch);
+                    gdst[h] = static_cast<uint32_t>(g - w.g_first) * static_cast<uint32_t>(a.out_gstride) +
+                              col_off(q, geo) + static_cast<uint32_t>(b * geo.sub);
+                    lsrc[h] = static_cast<uint32_t>(b * S::ROWB) + static_cast<uint32_t>(g * nq + q - w.col0) * 4u;
+                    break;
+                }
+                rem -= 8 * nch;
+            }
         }
     }
-    // Measurement-only store forms (tools/gen_fixed_kernels.py SH_GEN_STORE): 1 = one dword
-    // store per sub-block straight from the registers; 2 = the transposed dwordx4 form at
-    // 16-byte-aligned offsets (sub-block stride rounded up to 176: wrong bytes, alignment cost).
-    uint32_t dw_off;          // this lane's column offset (dword form)
-    __device__ __forceinline__ void store_row_dw(int y, const uint32_t (&w)[8]) const {
+    template <int YI>
+    __device__ __forceinline__ void row(int y, const uint32_t (&w)[8]) const {
+        uint8_t *im = img + (YI & 1) * S::P * S::SLOT;
 #pragma unroll
-        for (int b = 0; b < 8; ++b)
-            __builtin_amdgcn_raw_buffer_store_b32(w[b], rsrc, dw_off + static_cast<uint32_t>(b) * sub,
-                                                  static_cast<uint32_t>(y) * B, SH_STORE_AUX);
-    }
-    uint32_t sub;
-    __device__ __forceinline__ void store_row(int y, const uint32_t (&w)[8]) const {
-#pragma unroll
-        for (int b = 0; b < 8; ++b) reinterpret_cast<uint32_t *>(scr)[b * 64 + lane] = w[b];
+        for (int b = 0; b < 8; ++b) *reinterpret_cast<uint32_t *>(im + b * S::ROWB + wofs) = w[b];
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const int i = lane + 64 * h;
-            const u32x4 v = *reinterpret_cast<const u32x4 *>(scr + (i >> 4) * 256 + (i & 15) * 16);
-            __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, voff[h], static_cast<uint32_t>(y) * B, SH_STORE_AUX);
+            const u32x4 v = *reinterpret_cast<const u32x4 *>(im + lsrc[h]);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, gdst[h], static_cast<uint32_t>(y) * B, SH_STORE_AUX);
         }
+    }
+    template <int YI>
+    __device__ __forceinline__ void pad() const {
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
 };
 
@@ -304,7 +305,7 @@ struct Sink {
 // non-inlined body took `src` by reference through scratch and read the LDS ring with flat loads.
 template <class S, bool DEC>
 __device__ __forceinline__ int kernel_prologue(const FixedArgs &a, uint8_t *lds, Src<S, DEC> &src,
-                                               Sink &sink, long long col0, long long lo, long long hi) {
+                                               RowSink<S> &sink, long long col0, long long lo, long long hi) {
     WGInfo w;
     w.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     w.lane = threadIdx.x & 63;
@@ -321,9 +322,8 @@ __device__ __forceinline__ int kernel_prologue(const FixedArgs &a, uint8_t *lds,
     const int g = w.valid ? static_cast<int>(col / nq) : w.g_first;
     w.q = static_cast<int>(col - static_cast<long long>(g) * nq);
     w.gl = g - w.g_first;
-    // The store scratch (2 KB per wave) aliases the start of the ring: it is used only after the
+    // The row images of the epilogue alias the start of the ring: they are used only after the
     // last step, behind Src::release()'s barrier, so the ring gets that LDS as extra slots.
-    static_assert(S::R * S::SLOT >= S::NW * 2048, "scratch must fit inside the ring");
     uint8_t *lds_pos = lds + S::R * S::SLOT;
     if (DEC) {
         const int ng = a.groups_per_wg;
@@ -343,7 +343,7 @@ __device__ __forceinline__ int kernel_prologue(const FixedArgs &a, uint8_t *lds,
         __syncthreads();
     }
     src.init(a, w, lds, lds_pos);
-    sink.init(a, w, lds + w.wave * 2048);
+    sink.init(a, w, part, lds);
     return part;  // the generated body issues the ring's first DMAs
 }
 
@@ -387,7 +387,7 @@ inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArg
         extern __shared__ __attribute__((aligned(16))) uint8_t lds[];                             \
         using S = Shape<K, M, P, CW, R, DMA>;                                                     \
         Src<S, DEC> src;                                                                          \
-        Sink sink;                                                                                \
+        RowSink<S> sink;                                                                          \
         const long long c0 = static_cast<long long>(xcd_tile(blockIdx.x, gridDim.x)) * S::COLS;  \
         const int part = kernel_prologue<S, DEC>(a, lds, src, sink, c0, 0,                       \
                                                  static_cast<long long>(a.groups) * a.geo.nq);   \

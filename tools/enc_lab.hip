@@ -34,6 +34,83 @@ namespace lab {
 using namespace sh;
 using namespace sh::fixed;
 
+// Output, transposed through a per-wave 2 KB LDS scratch so every store is 16 contiguous bytes:
+// a lane holds word q of the 8 sub-blocks of a row; it writes them to scratch[b][lane], then
+// reads back two 16-byte items (sub-block b, 4-column chunk t) and stores each with one
+// buffer_store_dwordx4 -- 2 store instructions per row instead of 8 dword stores. A chunk lies
+// in one group (nq % 4 == 0) and is contiguous in memory (the shifted last chunk included).
+// Item i = lane + 64h (h = 0, 1): b = i / 16, t = i % 16. Chunks past the last group get an
+// out-of-range offset, dropped by the buffer unit.
+struct PieceSink {
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t voff[2];         // per item: chunk base + b * sub (or OOR)
+    uint32_t B;
+    uint8_t *scr;             // this wave's scratch [8][64] words
+    int lane;
+    __device__ __forceinline__ void init(const FixedArgs &a, const WGInfo &w, uint8_t *scratch) {
+        const Geometry &geo = a.geo;
+        rsrc = wg_rsrc(a.out, a.out_bytes, a.out_gstride, w.g_first);
+        B = geo.B;
+        lane = w.lane;
+        scr = scratch;
+        const int t = w.lane & 15;
+        const long long colx = w.col0 + (w.c - w.lane) + 4 * t;  // first column of chunk t
+        const int gx = colx >= 0 ? static_cast<int>(colx / geo.nq) : -1;
+        const int qx = static_cast<int>(colx - static_cast<long long>(gx) * geo.nq);
+        const uint32_t base = static_cast<uint32_t>(gx - w.g_first) * static_cast<uint32_t>(a.out_gstride) +
+                              col_off(qx, geo);
+        const bool ok = colx >= w.lo && colx < w.hi;
+#ifdef SH_GEN_STORE_ALIGNED  // measurement build only (see store_row_dw)
+        const uint32_t sstride = 176, abase = (static_cast<uint32_t>(gx - w.g_first) * static_cast<uint32_t>(a.out_gstride) + 4u * qx) & ~15u;
+#else
+        const uint32_t sstride = static_cast<uint32_t>(geo.sub), abase = base;
+#endif
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int b = (w.lane >> 4) + 4 * h;
+            voff[h] = ok ? abase + static_cast<uint32_t>(b) * sstride : OOR;
+        }
+        sub = static_cast<uint32_t>(geo.sub);
+        {
+            const long long colc = w.col0 + w.c;
+            const int gc = colc >= 0 ? static_cast<int>(colc / geo.nq) : -1;
+            const int qc = static_cast<int>(colc - static_cast<long long>(gc) * geo.nq);
+            dw_off = (colc >= w.lo && colc < w.hi)
+                         ? static_cast<uint32_t>(gc - w.g_first) * static_cast<uint32_t>(a.out_gstride) + col_off(qc, geo)
+                         : OOR;
+        }
+    }
+    // Measurement-only store forms (tools/gen_fixed_kernels.py SH_GEN_STORE): 1 = one dword
+    // store per sub-block straight from the registers; 2 = the transposed dwordx4 form at
+    // 16-byte-aligned offsets (sub-block stride rounded up to 176: wrong bytes, alignment cost).
+    uint32_t dw_off;          // this lane's column offset (dword form)
+    __device__ __forceinline__ void store_row_dw(int y, const uint32_t (&w)[8]) const {
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+            __builtin_amdgcn_raw_buffer_store_b32(w[b], rsrc, dw_off + static_cast<uint32_t>(b) * sub,
+                                                  static_cast<uint32_t>(y) * B, SH_STORE_AUX);
+    }
+    uint32_t sub;
+    __device__ __forceinline__ void store_row(int y, const uint32_t (&w)[8]) const {
+#pragma unroll
+        for (int b = 0; b < 8; ++b) reinterpret_cast<uint32_t *>(scr)[b * 64 + lane] = w[b];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int i = lane + 64 * h;
+            const u32x4 v = *reinterpret_cast<const u32x4 *>(scr + (i >> 4) * 256 + (i & 15) * 16);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, voff[h], static_cast<uint32_t>(y) * B, SH_STORE_AUX);
+        }
+    }
+    // the generated epilogue's interface (YI = the part's row index; pad = a part with fewer rows)
+    template <int YI>
+    __device__ __forceinline__ void row(int y, const uint32_t (&w)[8]) const { store_row(y, w); }
+    template <int YI>
+    __device__ __forceinline__ void pad() const {}
+};
+
+
+using Sink = PieceSink;
+
 #ifndef LAB_R
 #define LAB_R 16
 #endif
@@ -66,7 +143,18 @@ struct LabSrc : Src<S, false> {
     }
     template <int T, int I>
     __device__ __forceinline__ void wait() const {
-        Base::template wait<T, I>();
+        // persistent: the previous tile's 16 epilogue stores were issued after this tile's first
+        // R-1 DMAs, so a wait for one of those DMAs leaves the stores outstanding
+        if (PERS && prefetched && T < S::R - 1) {
+            constexpr int N = (I - T - 1) * S::DPW + 16;
+            static_assert(N < 64, "vmcnt");
+            if (S::NDMA % S::NW != 0 && this->wave * S::DPW >= S::NDMA)
+                asm volatile("s_barrier" ::: "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+        } else {
+            Base::template wait<T, I>();
+        }
         if (T == 3) st.put(1);  // the first wait of the schedule (S = 4)
         st.put(6 + T / 4);
     }
@@ -110,6 +198,22 @@ __device__ __forceinline__ uint32_t hwid() {
     return (xcc & 0xF) << 16 | (hw >> 8 & 0xFFFF);
 }
 
+// Timing-only (wrong results): each wave stores its rows as whole aligned 2 KB runs (the same
+// number of bytes as the product's output, in full 128-byte lines).
+struct ContigSink : Sink {
+    uint32_t cbase;
+    __device__ __forceinline__ void store_row(int y, const uint32_t (&w)[8]) const {
+#pragma unroll
+        for (int b = 0; b < 8; ++b) reinterpret_cast<uint32_t *>(scr)[b * 64 + lane] = w[b];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int i = lane + 64 * h;
+            const u32x4 v = *reinterpret_cast<const u32x4 *>(scr + (i >> 4) * 256 + (i & 15) * 16);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, cbase + h * 1024 + lane * 16, static_cast<uint32_t>(y & 7) * 2048u, 0);
+        }
+    }
+};
+
 // Timing-only (wrong results): every DMA source rounded down to 16 bytes.
 template <class L>
 __device__ __forceinline__ void align_src(L &src) {
@@ -118,12 +222,14 @@ __device__ __forceinline__ void align_src(L &src) {
         if (src.dbase[j] != OOR) src.dbase[j] &= ~15u;
 }
 
-// MODE 0: base (scratch aliases ring); 1: sep; 2: pers; 3: base with 16-byte-aligned DMA sources
+// MODE 0: base (scratch aliases ring); 1: sep; 2: pers; 3: base with 16-byte-aligned DMA sources;
+// 7: RowSink (row-assembled stores, correct results);
+// 4: base with ContigSink stores; 5: aligned DMA + ContigSink; 6: pers + aligned DMA + ContigSink
 template <int MODE, bool ST>
 __global__ __launch_bounds__(S::NT, 4) void kern(FixedArgs a, uint64_t *stamps, int ntiles) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint8_t *scratch = (MODE == 0 || MODE == 3) ? lds : lds + S::R * S::SLOT;
-    if (MODE != 2) {
+    if (MODE != 2 && MODE != 6) {
         const int tile = xcd_tile(blockIdx.x, gridDim.x);
         LabSrc<false, ST> src;
         src.st.p = stamps + static_cast<size_t>(tile) * NSTAMP;
@@ -132,8 +238,28 @@ __global__ __launch_bounds__(S::NT, 4) void kern(FixedArgs a, uint64_t *stamps, 
         src.has_next = false;
         Sink sink;
         const int part = prologue(a, lds, scratch, src, sink, static_cast<long long>(tile) * S::COLS);
-        if (MODE == 3) align_src(src);
-        run_k200_m32_enc(part, src, sink);
+        if (MODE == 3 || MODE == 5) align_src(src);
+        if (MODE == 7) {
+            RowSink<S> rs;
+            WGInfo w;
+            w.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+            w.lane = threadIdx.x & 63;
+            w.c = (w.wave / S::P) * 64 + w.lane;
+            w.col0 = static_cast<long long>(tile) * S::COLS;
+            w.lo = 0;
+            w.hi = static_cast<long long>(a.groups) * a.geo.nq;
+            w.g_first = static_cast<int>(w.col0 / a.geo.nq);
+            rs.init(a, w, part, lds);
+            run_k200_m32_enc(part, src, rs);
+        } else if (MODE >= 4) {
+            ContigSink cs;
+            static_cast<Sink &>(cs) = sink;
+            cs.rsrc = make_rsrc(a.out, static_cast<uint32_t>(a.out_bytes < 0x7FFFFFFFll ? a.out_bytes : 0x7FFFFFFFll));
+            cs.cbase = (static_cast<uint32_t>(tile) * S::NW + static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6))) * 16384u;
+            run_k200_m32_enc(part, src, cs);
+        } else {
+            run_k200_m32_enc(part, src, sink);
+        }
         src.st.put(3);
         if (ST && threadIdx.x == 0) stamps[static_cast<size_t>(tile) * NSTAMP + 4] = hwid() | (uint64_t)blockIdx.x << 32;
         return;
@@ -144,6 +270,7 @@ __global__ __launch_bounds__(S::NT, 4) void kern(FixedArgs a, uint64_t *stamps, 
     if (v >= ntiles) return;
     int tile = xcd_tile(v, ntiles);
     int part = prologue(a, lds, scratch, cur, sink, static_cast<long long>(tile) * S::COLS);
+    if (MODE == 6) align_src(cur);
     cur.prefetched = false;
     for (;;) {
         cur.st.p = stamps + static_cast<size_t>(tile) * NSTAMP;
@@ -152,7 +279,16 @@ __global__ __launch_bounds__(S::NT, 4) void kern(FixedArgs a, uint64_t *stamps, 
         const int tn = vn < ntiles ? xcd_tile(vn, ntiles) : -1;
         cur.has_next = tn >= 0;
         if (tn >= 0) prologue(a, lds, scratch, cur.nx, nsink, static_cast<long long>(tn) * S::COLS);
-        run_k200_m32_enc(part, cur, sink);
+        if (MODE == 6) {
+            if (tn >= 0) align_src(cur.nx);
+            ContigSink cs;
+            static_cast<Sink &>(cs) = sink;
+            cs.rsrc = make_rsrc(a.out, static_cast<uint32_t>(a.out_bytes < 0x7FFFFFFFll ? a.out_bytes : 0x7FFFFFFFll));
+            cs.cbase = (static_cast<uint32_t>(tile) * S::NW + static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6))) * 16384u;
+            run_k200_m32_enc(part, cur, cs);
+        } else {
+            run_k200_m32_enc(part, cur, sink);
+        }
         cur.st.put(3);
         if (ST && threadIdx.x == 0) stamps[static_cast<size_t>(tile) * NSTAMP + 4] = hwid() | (uint64_t)blockIdx.x << 32;
         if (tn < 0) break;
@@ -220,10 +356,20 @@ int main(int argc, char **argv) {
     std::vector<V> vs = {
         {"base", kern<0, false>, kern<0, true>, ring, ntiles},
 #ifdef LAB_MORE
-        {"sep", kern<1, false>, nullptr, ring + scr, ntiles},
         {"pers", kern<2, false>, kern<2, true>, ring + scr, 2 * cus},
 #endif
+#ifndef LAB_ONLY_PERS
+        {"sep", kern<1, false>, nullptr, ring + scr, ntiles},
         {"algn", kern<3, false>, kern<3, true>, ring, ntiles},
+#endif
+#ifndef LAB_ONLY_PERS
+        {"cstore", kern<4, false>, nullptr, ring, ntiles},
+        {"alcst", kern<5, false>, nullptr, ring, ntiles},
+#endif
+#ifdef LAB_MORE
+        {"palcst", kern<6, false>, nullptr, ring + scr, 2 * cus},
+#endif
+        {"rows", kern<7, false>, kern<7, true>, ring, ntiles},
     };
     printf("tiles %d, R %d, lds base %zu sep %zu, CUs %d\n", ntiles, S::R, ring, ring + scr, cus);
     for (auto &v : vs) {

@@ -273,8 +273,8 @@ def gen_config(k, m):
         for p, (y0, y1) in enumerate(parts):
             body = Body(k, rows, y0, y1).emit(R, sync, steps, KP)
             nr = y1 - y0
-            out.append(f"template <class Src>")
-            out.append(f"__device__ __forceinline__ void run_{name}_{mode}_p{p}(const Src &src, const Sink &sink) {{")
+            out.append(f"template <class Src, class Snk>")
+            out.append(f"__device__ __forceinline__ void run_{name}_{mode}_p{p}(const Src &src, const Snk &sink) {{")
             out.append(f"    uint32_t acc[{nr}][8];")
             # opaque zeros: a constant 0 would be folded into the first step, whose pinned results
             # then need register copies of shared table entries (AGPR spills at k=200).
@@ -283,20 +283,21 @@ def gen_config(k, m):
             out.append("    __builtin_amdgcn_sched_barrier(0);")
             out.append(f"    // epilogue: store rows {y0}..{y1 - 1}")
             out.append("    src.release();  // the store scratch aliases the ring")
-            for yi in range(nr):
+            nrmax = max(b - a for a, b in parts)
+            for yi in range(nrmax):  # every part joins the same number of row barriers
                 out.append("    __builtin_amdgcn_sched_barrier(0);")
-                if "halfstore" in ABLATE and p >= len(parts) // 2:
+                if yi >= nr:
+                    out.append(f"    sink.template pad<{yi}>();")
+                elif "halfstore" in ABLATE and p >= len(parts) // 2:
                     out.append(f"    asm volatile(\"\" :: " + ", ".join(f'"v"(acc[{yi}][{b}])' for b in range(8)) + ");")
-                elif os.environ.get("SH_GEN_STORE") == "1":
-                    out.append(f"    sink.store_row_dw({y0 + yi}, acc[{yi}]);")
                 elif "nostore" in ABLATE:
                     out.append(f"    asm volatile(\"\" :: " + ", ".join(f'"v"(acc[{yi}][{b}])' for b in range(8)) + ");")
                 else:
-                    out.append(f"    sink.store_row({y0 + yi}, acc[{yi}]);")
+                    out.append(f"    sink.template row<{yi}>({y0 + yi}, acc[{yi}]);")
             out.append("}")
             out.append("")
-        out.append(f"template <class Src>")
-        out.append(f"__device__ __forceinline__ void run_{name}_{mode}(int part, const Src &src, const Sink &sink) {{")
+        out.append(f"template <class Src, class Snk>")
+        out.append(f"__device__ __forceinline__ void run_{name}_{mode}(int part, const Src &src, const Snk &sink) {{")
         for p in range(len(parts)):
             kw = "if" if p == 0 else "else if"
             out.append(f"    {kw} (part == {p}) run_{name}_{mode}_p{p}(src, sink);")
