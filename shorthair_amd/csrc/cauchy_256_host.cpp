@@ -608,7 +608,7 @@ extern "C" int cauchy_256_profile(int capacity) {
     if (int rc = ensure_init(c)) return rc;
     std::lock_guard<std::mutex> g(c.mu);
     for (auto &q : c.evq)
-        for (hipEvent_t e : q) hipEventDestroy(e);
+        for (hipEvent_t e : q) (void)hipEventDestroy(e);
     c.evq.assign(std::max(0, capacity), {});
     for (auto &q : c.evq)
         for (hipEvent_t &e : q) SH_CHECK(hipEventCreate(&e));

@@ -115,7 +115,7 @@ using Sink = PieceSink;
 #define LAB_R 16
 #endif
 using S = Shape<200, 32, 4, 2, LAB_R, true>;
-constexpr int NSTAMP = 64;  // start, first, last, end, hwid, -, then one per ring wait (after its barrier)
+constexpr int NSTAMP = 96;  // + per wave (64 + 3*wave): s_memtime cycles computing, in vmcnt waits, in barrier waits  // start, first, last, end, hwid, -, then one per ring wait (after its barrier)
 
 __device__ __forceinline__ uint64_t now() { return __builtin_amdgcn_s_memrealtime(); }
 
@@ -141,8 +141,26 @@ struct LabSrc : Src<S, false> {
         if (PERS && prefetched && x < S::R - 1) return;
         Base::issue(x, pr);
     }
+    mutable uint64_t c_cmp = 0, c_dma = 0, c_bar = 0, c_last = 0;
     template <int T, int I>
     __device__ __forceinline__ void wait() const {
+        if (ST && !PERS) {  // split the wait: own DMAs (vmcnt), then the barrier
+            constexpr int N = (I - T - 1) * S::DPW;
+            uint64_t t0, t1, t2;
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+            if (S::NDMA % S::NW != 0 && this->wave * S::DPW >= S::NDMA)
+                asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+            else
+                asm volatile("s_waitcnt vmcnt(%1)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1) : "n"(N) : "memory");
+            asm volatile("s_barrier\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t2)::"memory");
+            if (T != 3) c_cmp += t0 - c_last;
+            c_dma += t1 - t0;
+            c_bar += t2 - t1;
+            c_last = t2;
+            if (T == 3) st.put(1);
+            st.put(6 + T / 4);
+            return;
+        }
         // persistent: the previous tile's 16 epilogue stores were issued after this tile's first
         // R-1 DMAs, so a wait for one of those DMAs leaves the stores outstanding
         if (PERS && prefetched && T < S::R - 1) {
@@ -160,6 +178,12 @@ struct LabSrc : Src<S, false> {
     }
     __device__ __forceinline__ void release() const {
         st.put(2);
+        if (ST && !PERS && (threadIdx.x & 63) == 0) {
+            uint64_t *q = st.p + 64 + 3 * this->wave;
+            q[0] = c_cmp;
+            q[1] = c_dma;
+            q[2] = c_bar;
+        }
         Base::release();  // every wave is past its last ring read
         if (PERS && has_next) {
             typename Base::Pre pr;
@@ -424,13 +448,15 @@ int main(int argc, char **argv) {
         snprintf(fn, sizeof fn, "gpurun_out/lab_stamps_%s.csv", v.name);
         FILE *f = fopen(fn, "w");
         if (f) {
-            fprintf(f, "tile,start,first,last,end,xcc,hwid,block,waits\n");
+            fprintf(f, "tile,start,first,last,end,xcc,hwid,block,waits,wavecyc\n");
             for (int t = 0; t < ntiles; ++t) {
                 const uint64_t *r = &h[(size_t)t * NSTAMP];
                 fprintf(f, "%d,%llu,%llu,%llu,%llu,%u,%u,%u,", t, (unsigned long long)r[0], (unsigned long long)r[1],
                         (unsigned long long)r[2], (unsigned long long)r[3], (unsigned)(r[4] >> 16 & 0xF),
                         (unsigned)(r[4] & 0xFFFF), (unsigned)(r[4] >> 32));
-                for (int j = 6; j < NSTAMP; ++j) fprintf(f, "%lld ", r[j] ? (long long)(r[j] - r[0]) : -1ll);
+                for (int j = 6; j < 56; ++j) fprintf(f, "%lld ", r[j] ? (long long)(r[j] - r[0]) : -1ll);
+                fprintf(f, ",");
+                for (int j = 64; j < 88; ++j) fprintf(f, "%llu ", (unsigned long long)r[j]);
                 fprintf(f, "\n");
             }
             fclose(f);
