@@ -13,7 +13,7 @@
 //
 // Two kernels: stageb_snip (generic path, any geometry; copy-and-XOR snippets, coefficients as
 // bytes) and stageb_fixed (after a compile-time stage A: accumulating snippets in VGPR-index
-// mode, setup-computed snippet addresses, LDS-staged residual tile). Group-uniform coefficients
+// mode, setup-computed snippet addresses, residual rows through a per-workgroup LDS-DMA ring). Group-uniform coefficients
 // require a wave to stay inside one group: at B = 1400 a group has 44 word columns.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -138,8 +138,7 @@ __global__ __launch_bounds__(256) void stageb_snip(StageBArgs a) {
 // (compacted: only the e rows that exist are staged and visited, so the work scales with e^2)
 // and, for every (i, j), the ABSOLUTE address of the snippet that applies M(S^-1[j][i])
 // (snippet 256 = return at once for zero / unused entries). The row loop therefore does no
-// scalar address arithmetic: per input row it takes the 8 sub-block words (loaded two rows
-// ahead), builds the
+// scalar address arithmetic: per input row it takes the 8 sub-block words (from the ring), builds the
 // two 4-bit window tables (reference win_encode tables, cauchy_256.cpp:1426-1445, 22 XORs) into
 // the pinned registers v[96:127], and makes 8 calls into the snippet table in VGPR-index mode
 // (accumulator set j at v[32+8j..]).
@@ -167,11 +166,6 @@ static_assert(SH_SNIPA_ACC == 32 && SH_SNIPA_T0 == 96 && SH_SNIPA_T1 == 112,
               "accumulating-snippet registers must match the asm constraints");
 static_assert(SH_SNIPA_STRIDE == SNIP_STRIDE && SH_SNIPA_NULL == SNIP_NULL, "snippet table layout");
 
-// No LDS tile: each wave loads its own residual rows with buffer loads, prefetched two rows ahead
-// into registers and waited for with its own vmcnt (no barrier, no serialized tile prologue),
-// so occupancy is set by registers (4 waves per SIMD). The waves of a group read the same rows
-// (L2 hits after the first). Measured against an LDS-staged tile (48 KB per workgroup, 3 per
-// CU): 0.40 vs 0.42 ms at the headline, and no LDS limit for large e (Shorthair's m = 56, 66).
 #define SH_ROW_ASM_R                                                                              \
     "v_mov_b32 v97, %[d0]\n"                                                                      \
     "v_mov_b32 v98, %[d1]\n"                                                                      \
@@ -239,7 +233,20 @@ __device__ __forceinline__ void row_regs(const Row8 &d, const uint64_t (&tg)[8],
                    "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "s40", "s41", "m0", "memory");
 }
 
+// The residual rows are staged in one LDS ring per workgroup (one group, 64-column
+// chunk): each row is fetched ONCE per workgroup by LDS-DMA (2 KB: waves 0 and 1 issue one 1 KB
+// piece each) instead of once per wave, with up to 12 rows in flight per workgroup. Rows in groups
+// of RB_S: before a group every wave waits for its own DMAs of it (counted vmcnt, constant in the
+// steady state) and joins the barrier, which also frees the slots of the previous group; they are
+// refilled right there. Waves without outputs (8 * wave >= e) join the barriers and compute nothing.
+// Measured at the headline (8192 groups, e = 32): 0.360 vs 0.377-0.384 ms for waves that each
+// loaded their own rows two rows ahead into registers (round 2's form; an LDS tile of the whole
+// residual loaded up front, 48 KB per workgroup, took 0.42 ms).
+constexpr int RB_R = 16, RB_S = 4, RB_ROW = 8 * 64 * 4;
+static_assert(RB_R == 4 * RB_S, "steady state: the slots of one group are refilled per group");
+
 __global__ __launch_bounds__(256, 4) void stageb_fixed(StageBFixedArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[RB_R * RB_ROW];
     const Geometry geo = a.geo;
     const int ncc = (geo.nq + 63) / 64;
     const int g = blockIdx.x / ncc;
@@ -249,76 +256,62 @@ __global__ __launch_bounds__(256, 4) void stageb_fixed(StageBFixedArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int e = a.e[g];
+    if (e <= 0) return;  // uniform over the workgroup
     const int j0 = (blockIdx.y * 4 + wave) * 8;
-    if (j0 >= e) return;  // wave-uniform; e <= 0 included
-    // idle lanes (lane >= ncols) load a valid column of the group and store nothing
-    const uint32_t col = colx_off(c0 + min(lane, ncols - 1), geo.nq, geo.sub);
-    uint32_t voff[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s) voff[s] = col + static_cast<uint32_t>(s) * geo.sub;
+    const bool active = j0 < e;
     const long long gbase = static_cast<long long>(g) * a.in_gstride;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.in + gbase), static_cast<short>(0), static_cast<int>(a.in_gstride), 0x00020000);
-    // scalar loads (gfx950 has no sub-dword s_load: read the row list as dwords)
+    // DMA piece of waves 0 and 1: slot bytes [wave*1024 + lane*16, +16) = sub-block sa, columns
+    // c0 + cq .. + 3 (a whole 4-column chunk: nq % 4 == 0); chunks past the group read zeros
+    const int off = wave * 1024 + lane * 16;
+    const int sa = off / 256, cq = (off % 256) / 4;
+    const uint32_t dsrc = (c0 + cq < geo.nq) ? colx_off(c0 + cq, geo.nq, geo.sub) + static_cast<uint32_t>(sa * geo.sub)
+                                             : 0x80000000u;
     typedef const __attribute__((address_space(4))) uint32_t cu32_t;
     typedef const __attribute__((address_space(4))) uint64_t cu64_t;
-    const cu32_t *rr = (const cu32_t *)(a.rrow + static_cast<long long>(g) * a.ldR);  // ldR % 4 == 0
+    const cu32_t *rr = (const cu32_t *)(a.rrow + static_cast<long long>(g) * a.ldR);
     const cu64_t *tp = (const cu64_t *)(a.targets + (static_cast<long long>(g) * (a.ldT / 8) + (j0 >> 3)) * a.emax * 8);
     const int elast = e - 1;
-    auto row_of = [&](int i) { return min(i, elast); };  // prefetches past the end re-read the last row
-    auto row_soff = [&](int i) {
-        i = row_of(i);
-        return ((rr[i >> 2] >> (8 * (i & 3))) & 0xFFu) * static_cast<uint32_t>(geo.B);
+    auto issue = [&](int i) {  // row i into slot i % RB_R (rows past the end re-read the last row)
+        if (wave < 2) {
+            const int x = min(i, elast);
+            const uint32_t soff = ((rr[x >> 2] >> (8 * (x & 3))) & 0xFFu) * static_cast<uint32_t>(geo.B);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(ring + (i % RB_R) * RB_ROW + wave * 1024),
+                                                     16, dsrc, soff, 0, 0);
+        }
     };
-    auto load_row = [&](uint32_t soff, Row8 &d) {
-#pragma unroll
-        for (int s = 0; s < 8; ++s) d.w[s] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff[s], soff, 0);
-    };
-
     u32x16 a01, a23, a45, a67;
 #pragma unroll
     for (int t = 0; t < 16; ++t) a01[t] = a23[t] = a45[t] = a67[t] = 0;
     uint32_t z0 = 0, z1 = 0;
-    Row8 r0, r1, r2;
-    load_row(row_soff(0), r0);
-    load_row(row_soff(1), r1);
-    int i = 0;
-    for (; i + 3 <= e; i += 3) {  // rows i, i+1, i+2 in r0, r1, r2 (rotating, two rows in flight)
-        // the three rows' snippet addresses and the next three row offsets in one batch of scalar
-        // loads: scalar loads return out of order, so any wait for one of them waits for all
-        // (one exposed latency per 3 rows). The row loads are unconditional (indices clamped to
-        // the last row, re-reads are L2 hits) so the counted vmcnt waits stay two rows deep.
-        const int i2 = row_of(i + 2), i3 = row_of(i + 3), i4 = row_of(i + 4);
-        const uint32_t w2 = rr[i2 >> 2], w3 = rr[i3 >> 2], w4 = rr[i4 >> 2];
-        uint64_t tg[3][8];
+    for (int i = 0; i < RB_R - RB_S; ++i) issue(i);
+    const int ngroups = (e + RB_S - 1) / RB_S;
+    for (int ig = 0; ig < ngroups; ++ig) {
+        // own DMAs of rows 4ig..4ig+3 landed (RB_R - 2 * RB_S younger ones may be outstanding)
+        if (wave < 2)
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(RB_R - 2 * RB_S) : "memory");
+        else
+            asm volatile("s_barrier" ::: "memory");
 #pragma unroll
-        for (int r = 0; r < 3; ++r) {
-            const int x = row_of(i + r);
+        for (int r = 0; r < RB_S; ++r) issue(ig * RB_S + RB_R - RB_S + r);
+        if (!active) continue;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) tg[r][j] = tp[x * 8 + j];
-        }
-        auto pick = [&](uint32_t w, int x) { return ((w >> (8 * (x & 3))) & 0xFFu) * static_cast<uint32_t>(geo.B); };
-        const uint32_t s2 = pick(w2, i2), s3 = pick(w3, i3), s4 = pick(w4, i4);
-        load_row(s2, r2);
-        row_regs(r0, tg[0], a01, a23, a45, a67, z0, z1);
-        load_row(s3, r0);
-        row_regs(r1, tg[1], a01, a23, a45, a67, z0, z1);
-        load_row(s4, r1);
-        row_regs(r2, tg[2], a01, a23, a45, a67, z0, z1);
-    }
-    if (i < e) {  // one or two rows left, in r0 (and r1)
-        uint64_t tg[8];
+        for (int r = 0; r < RB_S; ++r) {
+            const int i = ig * RB_S + r;
+            if (i >= e) break;  // uniform
+            uint64_t tg[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) tg[j] = tp[row_of(i) * 8 + j];
-        row_regs(r0, tg, a01, a23, a45, a67, z0, z1);
-        if (i + 1 < e) {
+            for (int j = 0; j < 8; ++j) tg[j] = tp[i * 8 + j];
+            const uint8_t *slot = ring + (i % RB_R) * RB_ROW + lane * 4;
+            Row8 d;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) tg[j] = tp[row_of(i + 1) * 8 + j];
-            row_regs(r1, tg, a01, a23, a45, a67, z0, z1);
+            for (int s = 0; s < 8; ++s) d.w[s] = *reinterpret_cast<const uint32_t *>(slot + s * 256);
+            row_regs(d, tg, a01, a23, a45, a67, z0, z1);
         }
     }
-
-    if (lane >= ncols) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no ring DMA may land after the workgroup ends
+    if (!active || lane >= ncols) return;
     uint32_t acc[8][8];
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
