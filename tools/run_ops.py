@@ -22,6 +22,7 @@ def main():
     p.add_argument("--groups", type=int, default=8192)
     p.add_argument("--erasures", type=int, default=32)
     p.add_argument("--concurrent", action="store_true", help="encode and decode on two streams at once")
+    p.add_argument("--zero", action="store_true", help="all-zero data blocks (data-dependent power / DVFS check)")
     a = p.parse_args()
     import torch
     import shorthair_amd as sh
@@ -30,6 +31,8 @@ def main():
     data = torch.empty((G, k, B), dtype=torch.uint8, device="cuda")
     rec = torch.empty((G, m, B), dtype=torch.uint8, device="cuda")
     sh.fill_synthetic(data, k, B, G, 0, 0xBE)
+    if a.zero:
+        data.zero_()
     sh.encode_batch(k, m, B, G, data, rec)
     if a.op in ("decode", "both"):
         rows = np.zeros((G, k), np.uint8)
