@@ -55,9 +55,12 @@ int cauchy_256_batch_reserve_stream(int k, int m, int block_bytes, int groups, v
 
 /* Malformed decode groups (more recovery blocks than erased originals: duplicate rows, outside
  * the reference's contract) are left untouched, counted, and flagged with d_out_count[g] = -1 by
- * cauchy_256_decode_batch_out. This waits for `stream` and returns the number of such groups
- * since the previous call (resetting the count), or -2 on a GPU error. The single-group
- * cauchy_256_decode returns -1 for such a group. */
+ * cauchy_256_decode_batch_out. Counts are kept per stream: this waits for `stream` and returns the
+ * number of such groups among the decodes enqueued on `stream` since the previous call for that
+ * stream (read and reset in stream order), or -2 on a GPU error. The single-group
+ * cauchy_256_decode returns -1 for such a group (it decodes on cauchy_256_default_stream()).
+ * Every entry point runs on the library's device and restores the calling thread's current HIP
+ * device before it returns. */
 int cauchy_256_batch_errors(void *stream);
 
 /* Synthetic workload: block x of group g0+g = PCG32 Seed((g0+g)*256 + x, cfg) words (the same

@@ -12,6 +12,8 @@
 #include <algorithm>
 #include <cstring>
 #include <array>
+#include <atomic>
+#include <memory>
 #include <map>
 #include <mutex>
 #include <utility>
@@ -77,13 +79,22 @@ struct PinnedBuf {
     }
 };
 
+// Per-stream decode state: the workspace and the malformed-group counter of the decodes enqueued
+// on that stream. `mu` is held from the workspace lookup until the call's kernels are enqueued, so a
+// concurrent grow (another thread on the same stream, or cauchy_256_batch_reserve_stream) can never
+// free a buffer that a call is about to use; calls on one stream are then ordered by the stream.
+struct StreamState {
+    std::mutex mu;
+    DevBuf ws;
+    int *d_errors = nullptr;
+};
+
 struct Context {
-    std::mutex mu;          // guards lazy state (tables, caches, workspaces, profiling events)
+    std::mutex mu;          // guards lazy state (tables, caches, the stream map, profiling events)
     bool ready = false;
     int device = 0;
     hipStream_t stream = nullptr;
     uint64_t snip_base = 0;           // stage-B snippet table address (code object)
-    int *d_errors = nullptr;          // malformed-group counter (decode setup)
     uint64_t *d_rowbytes = nullptr;   // 256 x 8 bytes
     uint8_t *d_exp = nullptr;         // 512
     uint16_t *d_log = nullptr;        // 256
@@ -91,10 +102,9 @@ struct Context {
     // followed by the raw (m-1) x k rows 1..m-1 and the Cauchy parameters X'[k], Y'[m] for
     // decode setup.
     std::map<std::pair<int, int>, uint8_t *> gens;
-    // Decode workspace per stream: two decodes in flight on different streams never share
-    // scratch; calls on one stream are ordered by the stream itself.
-    std::map<hipStream_t, DevBuf> ws;
-    size_t ws_reserve = 0;            // cauchy_256_batch_reserve: minimum size of a new workspace
+    // Decode state per stream: two decodes in flight on different streams never share scratch.
+    std::map<hipStream_t, std::unique_ptr<StreamState>> streams;
+    std::atomic<size_t> ws_reserve{0};  // cauchy_256_batch_reserve: minimum size of a workspace
     // stage timing (cauchy_256_profile): per profiled decode, events around setup / stage A /
     // stage B, in a ring of `evq.size()` quadruples (no host synchronisation while recording)
     std::vector<std::array<hipEvent_t, 4>> evq;
@@ -133,32 +143,67 @@ int init_locked(Context &c, int device) {
     SH_CHECK(hipMemcpy(c.d_exp, f.exp, 512, hipMemcpyHostToDevice));
     SH_CHECK(hipMalloc(&c.d_log, 512));
     SH_CHECK(hipMemcpy(c.d_log, f.log, 512, hipMemcpyHostToDevice));
-    SH_CHECK(hipMalloc(&c.d_errors, sizeof(int)));
-    SH_CHECK(hipMemset(c.d_errors, 0, sizeof(int)));
     SH_CHECK(sh::stageb_snip_base(&c.snip_base, c.stream));
     c.device = device;
     c.ready = true;
     return 0;
 }
 
-// Every entry point runs on the library's device, whatever the calling thread had current
-// (HIP's current device is per thread; allocations and launches follow it).
-int ensure_init(Context &c) {
-    {
-        std::lock_guard<std::mutex> g(c.mu);
-        if (int rc = init_locked(c, c.device)) return rc;
+// Every entry point runs on the library's device, whatever the calling thread had current (HIP's
+// current device is per thread; allocations and launches follow it), and gives the thread its
+// previous device back when it returns: construct one at the top of each entry point.
+struct DeviceScope {
+    int rc = 0, prev = -1, dev = -1;
+    explicit DeviceScope(Context &c) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        {
+            std::lock_guard<std::mutex> g(c.mu);
+            rc = init_locked(c, c.device);
+        }
+        if (rc) return;
+        dev = c.device;
+        if (prev != dev && hipSetDevice(dev) != hipSuccess) {
+            std::fprintf(stderr, "libcauchy256: hipSetDevice(%d) failed\n", dev);
+            rc = -2;
+        }
     }
-    int cur = -1;
-    if (hipGetDevice(&cur) != hipSuccess || cur != c.device) SH_CHECK(hipSetDevice(c.device));
-    return 0;
+    ~DeviceScope() {
+        if (prev >= 0 && dev >= 0 && prev != dev) (void)hipSetDevice(prev);
+    }
+    DeviceScope(const DeviceScope &) = delete;
+    DeviceScope &operator=(const DeviceScope &) = delete;
+};
+
+// The decode state of `stream` (created on first use, never destroyed: the map owns it).
+StreamState *stream_state(Context &c, hipStream_t stream) {
+    std::lock_guard<std::mutex> g(c.mu);
+    auto &slot = c.streams[stream];
+    if (!slot) {
+        auto st = std::make_unique<StreamState>();
+        if (hipMalloc(&st->d_errors, sizeof(int)) != hipSuccess) return nullptr;
+        if (hipMemset(st->d_errors, 0, sizeof(int)) != hipSuccess) return nullptr;
+        slot = std::move(st);
+    }
+    return slot.get();
 }
 
-// Workspace of `stream`, grown to at least `bytes` (under c.mu).
-uint8_t *workspace(Context &c, hipStream_t stream, size_t bytes) {
-    std::lock_guard<std::mutex> g(c.mu);
-    DevBuf &b = c.ws[stream];
-    if (b.ensure(std::max(bytes, c.ws_reserve), stream)) return nullptr;
-    return static_cast<uint8_t *>(b.p);
+// A stream's workspace, locked for one call: at least `bytes` (and the reserve), valid while the
+// lease lives. Kernels enqueued under the lease are ordered before any later grow's free by the
+// grow's stream synchronisation.
+struct WsLease {
+    std::unique_lock<std::mutex> lk;
+    uint8_t *p = nullptr;
+    int *errors = nullptr;
+};
+
+int lease_workspace(Context &c, hipStream_t stream, size_t bytes, WsLease &out) {
+    StreamState *st = stream_state(c, stream);
+    if (!st) return -2;
+    out.lk = std::unique_lock<std::mutex>(st->mu);
+    if (st->ws.ensure(std::max(bytes, c.ws_reserve.load()), stream)) return -2;
+    out.p = static_cast<uint8_t *>(st->ws.p);
+    out.errors = st->d_errors;
+    return 0;
 }
 
 // Device generator for (k, m), m >= 2, k + m <= 256. Cached; created once per shape.
@@ -210,7 +255,8 @@ hipError_t launch_fixed_batch(int k, int m, int B, int groups, const uint8_t *in
 int encode_batch(int k, int m, int B, int groups, const uint8_t *d_in, uint8_t *d_out,
                  hipStream_t s) {
     Context &c = ctx();
-    if (int rc = ensure_init(c)) return rc;
+    DeviceScope ds(c);
+    if (ds.rc) return ds.rc;
     if (groups <= 0 || m <= 0 || k <= 0 || B <= 0) return 0;
     const long long in_gs = static_cast<long long>(k) * B, out_gs = static_cast<long long>(m) * B;
     if (k <= 1) {  // reference cauchy_256.cpp:1485-1493
@@ -346,7 +392,7 @@ hipError_t launch_stage_b(const DecodeWS &w, int n_in, int B, int groups, uint8_
 // Common decode core (m >= 2, valid params): writes recovered blocks densely into `dst`
 // ([G][emax][B]) and leaves per-group e / rec_idx / erasures in the workspace.
 int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_blocks,
-                const uint8_t *d_rows, DecodeWS &w, uint8_t *dst, hipStream_t s) {
+                const uint8_t *d_rows, DecodeWS &w, int *errors, uint8_t *dst, hipStream_t s) {
     uint8_t *gen = generator(c, k, m);
     if (!gen) return -2;
     sh::DecodeSetupArgs sa{};
@@ -375,7 +421,7 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
     sa.ldR = round4(w.emax);
     sa.targets = w.targets;
     sa.snip_base = c.snip_base;
-    sa.errors = c.d_errors;
+    sa.errors = errors;
     hipEvent_t *ev = nullptr;
     {  // check and claim the slot in one critical section (profile() may resize the ring)
         std::lock_guard<std::mutex> g(c.mu);
@@ -433,10 +479,13 @@ int invalid_decode_status(int k, int groups, const uint8_t *d_rows, hipStream_t 
     return 0;
 }
 
+// e_host (optional, pinned host memory): receives group 0's e, copied on `s` while the workspace
+// is still leased to this call (the single-group ABI reads it after synchronising).
 int decode_batch(int k, int m, int B, int groups, uint8_t *d_blocks, uint8_t *d_rows,
-                 hipStream_t s) {
+                 hipStream_t s, int *e_host = nullptr) {
     Context &c = ctx();
-    if (int rc = ensure_init(c)) return rc;
+    DeviceScope ds(c);
+    if (ds.rc) return ds.rc;
     if (groups <= 0 || k <= 0) return 0;
     if (k <= 1) {  // cauchy_256.cpp:1236-1240
         SH_CHECK(sh::launch_decode_k1(d_rows, k, groups, s));
@@ -448,10 +497,10 @@ int decode_batch(int k, int m, int B, int groups, uint8_t *d_blocks, uint8_t *d_
     }
     if (k + m > 256 || B % 8 != 0) return invalid_decode_status(k, groups, d_rows, s);
     DecodeWS w{};
-    uint8_t *wsp = workspace(c, s, carve(w, nullptr, k, m, B, groups, true));
-    if (!wsp) return -2;
-    carve(w, wsp, k, m, B, groups, true);
-    if (int rc = decode_core(c, k, m, B, groups, d_blocks, d_rows, w, w.recovered, s)) return rc;
+    WsLease ls;
+    if (int rc = lease_workspace(c, s, carve(w, nullptr, k, m, B, groups, true), ls)) return rc;
+    carve(w, ls.p, k, m, B, groups, true);
+    if (int rc = decode_core(c, k, m, B, groups, d_blocks, d_rows, w, ls.errors, w.recovered, s)) return rc;
     sh::ScatterArgs sc{};
     sc.src = w.recovered;
     sc.src_gstride = static_cast<long long>(w.emax) * B;
@@ -465,6 +514,7 @@ int decode_batch(int k, int m, int B, int groups, uint8_t *d_blocks, uint8_t *d_
     sc.emax = w.emax;
     sc.B = B;
     SH_CHECK(sh::launch_scatter(sc, groups, s));
+    if (e_host) SH_CHECK(hipMemcpyAsync(e_host, w.e, sizeof(int), hipMemcpyDeviceToHost, s));
     return 0;
 }
 
@@ -496,17 +546,18 @@ extern "C" int cauchy_256_decode_batch_out(int k, int m, int block_bytes, int gr
                                            void *d_out, unsigned char *d_out_rows,
                                            int *d_out_count, void *stream) {
     Context &c = ctx();
-    if (int rc = ensure_init(c)) return rc;
+    DeviceScope ds(c);
+    if (ds.rc) return ds.rc;
     if (groups <= 0) return 0;
     if (k < 2 || m < 2) return -1;
     hipStream_t s = pick(stream);
     if (k + m > 256 || block_bytes % 8 != 0) return invalid_decode_status(k, groups, d_rows, s);
     DecodeWS w{};
-    uint8_t *wsp = workspace(c, s, carve(w, nullptr, k, m, block_bytes, groups, false));
-    if (!wsp) return -2;
-    carve(w, wsp, k, m, block_bytes, groups, false);
+    WsLease ls;
+    if (int rc = lease_workspace(c, s, carve(w, nullptr, k, m, block_bytes, groups, false), ls)) return rc;
+    carve(w, ls.p, k, m, block_bytes, groups, false);
     if (int rc = decode_core(c, k, m, block_bytes, groups, static_cast<const uint8_t *>(d_blocks),
-                             d_rows, w, static_cast<uint8_t *>(d_out), s))
+                             d_rows, w, ls.errors, static_cast<uint8_t *>(d_out), s))
         return rc;
     SH_CHECK(hipMemcpyAsync(d_out_rows, w.erasures, static_cast<size_t>(groups) * w.emax,
                             hipMemcpyDeviceToDevice, s));
@@ -521,33 +572,50 @@ extern "C" int cauchy_256_batch_reserve(int k, int m, int block_bytes, int group
 
 extern "C" int cauchy_256_batch_reserve_stream(int k, int m, int block_bytes, int groups, void *stream) {
     Context &c = ctx();
-    if (int rc = ensure_init(c)) return rc;
+    DeviceScope ds(c);
+    if (ds.rc) return ds.rc;
     if (k < 2 || m < 2 || k + m > 256 || block_bytes <= 0 || groups <= 0) return 0;
     DecodeWS w{};
     const size_t need = carve(w, nullptr, k, m, block_bytes, groups, true);
     if (!generator(c, k, m)) return -2;
-    {
-        std::lock_guard<std::mutex> g(c.mu);
-        c.ws_reserve = std::max(c.ws_reserve, need);
+    size_t cur = c.ws_reserve.load();
+    while (cur < need && !c.ws_reserve.compare_exchange_weak(cur, need)) {
     }
-    return workspace(c, pick(stream), need) ? 0 : -2;
+    WsLease ls;
+    return lease_workspace(c, pick(stream), need, ls);
 }
 
 extern "C" int cauchy_256_batch_errors(void *stream) {
     Context &c = ctx();
-    if (int rc = ensure_init(c)) return rc;
-    SH_CHECK(hipStreamSynchronize(pick(stream)));
-    int n = 0;
-    SH_CHECK(hipMemcpy(&n, c.d_errors, sizeof(int), hipMemcpyDeviceToHost));
-    SH_CHECK(hipMemset(c.d_errors, 0, sizeof(int)));
-    return n;
+    DeviceScope ds(c);
+    if (ds.rc) return ds.rc;
+    hipStream_t s = pick(stream);
+    StreamState *st = stream_state(c, s);
+    if (!st) return -2;
+    // Read and clear in stream order, under the stream's lock: a decode enqueued on this stream
+    // (by any thread) lands either before the read or after the clear, never in between.
+    std::lock_guard<std::mutex> g(st->mu);
+    int *n = nullptr;
+    SH_CHECK(hipHostMalloc(reinterpret_cast<void **>(&n), sizeof(int), hipHostMallocDefault));
+    *n = 0;
+    hipError_t e = hipMemcpyAsync(n, st->d_errors, sizeof(int), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemsetAsync(st->d_errors, 0, sizeof(int), s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    const int r = *n;
+    (void)hipHostFree(n);
+    if (e != hipSuccess) {
+        std::fprintf(stderr, "libcauchy256: batch_errors failed: %s\n", hipGetErrorString(e));
+        return -2;
+    }
+    return r;
 }
 
 extern "C" int cauchy_256_fill_synthetic(void *d_out, int n, int block_bytes, int groups,
                                          unsigned long long g0, unsigned long long cfg,
                                          void *stream) {
     Context &c = ctx();
-    if (int rc = ensure_init(c)) return rc;
+    DeviceScope ds(c);
+    if (ds.rc) return ds.rc;
     SH_CHECK(sh::launch_fill(static_cast<uint8_t *>(d_out), static_cast<long long>(n) * block_bytes,
                              n, block_bytes, groups, g0, cfg, pick(stream)));
     return 0;
@@ -599,13 +667,15 @@ extern "C" int cauchy_256_batch_path(int k, int m, int block_bytes) {
 
 extern "C" void *cauchy_256_default_stream(void) {
     Context &c = ctx();
-    if (ensure_init(c)) return nullptr;
+    DeviceScope ds(c);
+    if (ds.rc) return nullptr;
     return c.stream;
 }
 
 extern "C" int cauchy_256_profile(int capacity) {
     Context &c = ctx();
-    if (int rc = ensure_init(c)) return rc;
+    DeviceScope ds(c);
+    if (ds.rc) return ds.rc;
     std::lock_guard<std::mutex> g(c.mu);
     for (auto &q : c.evq)
         for (hipEvent_t e : q) (void)hipEventDestroy(e);
@@ -636,7 +706,8 @@ extern "C" int cauchy_256_profile_read(float *ms) {
 
 extern "C" int cauchy_256_sync(void *stream) {
     Context &c = ctx();
-    if (int rc = ensure_init(c)) return rc;
+    DeviceScope ds(c);
+    if (ds.rc) return ds.rc;
     SH_CHECK(hipStreamSynchronize(pick(stream)));
     return 0;
 }
@@ -654,7 +725,8 @@ extern "C" int _cauchy_256_init(int expected_version) {
 extern "C" int cauchy_256_encode(int k, int m, const unsigned char *data_ptrs[],
                                  void *recovery_blocks, int block_bytes) {
     Context &c = ctx();
-    if (int rc = ensure_init(c)) return rc;
+    DeviceScope ds(c);
+    if (ds.rc) return ds.rc;
     if (k <= 0 || m <= 0 || block_bytes <= 0) return 0;
     const int kin = k <= 1 ? 1 : k;
     const size_t in_bytes = static_cast<size_t>(kin) * block_bytes;
@@ -678,7 +750,8 @@ extern "C" int cauchy_256_encode(int k, int m, const unsigned char *data_ptrs[],
 
 extern "C" int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes) {
     Context &c = ctx();
-    if (int rc = ensure_init(c)) return rc;
+    DeviceScope ds(c);
+    if (ds.rc) return ds.rc;
     if (k <= 1) {  // cauchy_256.cpp:1236-1240: no data touched
         if (k == 1) blocks[0].row = 0;
         return 0;
@@ -686,7 +759,7 @@ extern "C" int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes) {
     if (block_bytes <= 0) return 0;
     const size_t data_bytes = static_cast<size_t>(k) * block_bytes;
     std::lock_guard<std::mutex> g(c.stage_mu);
-    if (int rc = c.h_stage.ensure(data_bytes + 256)) return rc;
+    if (int rc = c.h_stage.ensure(data_bytes + 256 + 8)) return rc;
     if (int rc = c.d_stage.ensure(data_bytes + 256)) return rc;
     uint8_t *h = static_cast<uint8_t *>(c.h_stage.p);
     uint8_t *d = static_cast<uint8_t *>(c.d_stage.p);
@@ -694,18 +767,15 @@ extern "C" int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes) {
         std::memcpy(h + static_cast<size_t>(i) * block_bytes, blocks[i].data, block_bytes);
         h[data_bytes + i] = blocks[i].row;
     }
+    // pinned word for the group's e, past the rows (the decode core fills it when it runs)
+    int *e_host = reinterpret_cast<int *>(h + ((data_bytes + k + 3) & ~static_cast<size_t>(3)));
+    *e_host = 0;
     SH_CHECK(hipMemcpyAsync(d, h, data_bytes + k, hipMemcpyHostToDevice, c.stream));
-    const int rc = decode_batch(k, m, block_bytes, 1, d, d + data_bytes, c.stream);
+    const int rc = decode_batch(k, m, block_bytes, 1, d, d + data_bytes, c.stream, e_host);
     if (rc != 0) return rc;
     SH_CHECK(hipMemcpyAsync(h, d, data_bytes + k, hipMemcpyDeviceToHost, c.stream));
-    int e = 0;
-    if (m >= 2 && k + m <= 256 && block_bytes % 8 == 0) {
-        // the decode core ran: the group's e is the first word of this stream's workspace (carve)
-        const uint8_t *wsp = workspace(c, c.stream, 0);
-        if (!wsp) return -2;
-        SH_CHECK(hipMemcpyAsync(&e, wsp, sizeof(int), hipMemcpyDeviceToHost, c.stream));
-    }
     SH_CHECK(hipStreamSynchronize(c.stream));
+    const int e = *e_host;
     // A group with more recovery blocks than erasures (outside the reference's contract: its
     // rows would be duplicates) is left untouched and reported as invalid.
     if (e < 0) return -1;

@@ -488,7 +488,9 @@ __global__ __launch_bounds__(64) void stageb_small(StageBSmallArgs a) {
     const uint8_t *cp = a.coefT + static_cast<long long>(g) * a.coefT_gstride + j0;
     const uint32_t lane4 = static_cast<uint32_t>(lane) * 4u;
     auto load = [&](int i, uint32_t (&d)[8], uint64_t &cc) {
-        const int r = rrs[gs][min(i, max(el - 1, 0))];
+        // lanes past the wave's last group (gs >= gpw, or past the batch) read row 0 of group g0:
+        // their rrs row was never written, and any other row could lie past the workspace
+        const int r = valid ? rrs[gs][min(i, max(el - 1, 0))] : 0;
         const uint8_t *p = res + static_cast<long long>(r) * geo.B;
 #pragma unroll
         for (int s = 0; s < 8; ++s) __builtin_memcpy(&d[s], p + s * geo.sub, 4);
