@@ -354,7 +354,9 @@ def packet_groups(args, k, m, B):
 # (Shorthair.cpp:502-504 clamps m to 256-k).
 SWEEP = [("C2", 64, 16, 1400)] + [("C4", k, m, B) for (k, m) in ((28, 4), (112, 16), (224, 32))
                                   for B in (256, 1400, 65536)] + \
-        [("tester", 200, 56, 1352), ("tester", 190, 66, 1336), ("tester", 190, 66, 1344)]
+        [("tester", 200, 56, 1352), ("tester", 190, 66, 1336), ("tester", 190, 66, 1344)] + \
+        [("off-grid", 120, 136, 1400), ("off-grid", 150, 40, 1400), ("off-grid", 50, 10, 1000),
+         ("off-grid", 180, 76, 1352)]
 
 
 def sweep(args, sh, torch, s):
@@ -366,7 +368,7 @@ def sweep(args, sh, torch, s):
         data = torch.empty((G, k, B), dtype=torch.uint8, device="cuda")
         rec = torch.empty((G, m, B), dtype=torch.uint8, device="cuda")
         sh.fill_synthetic(data, k, B, G, 0, 0x5E, s)
-        r = {"config": tag, "k": k, "m": m, "B": B, "groups": G, "path": "fixed" if sh.has_fixed(k, m, B) else "generic"}
+        r = {"config": tag, "k": k, "m": m, "B": B, "groups": G, "path": sh.path(k, m, B)}
         r.update(_time_ops(args, sh, torch, s, k, m, B, G, data, rec, min(k, m)))
         out.append(r)
         del data, rec

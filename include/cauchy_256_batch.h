@@ -76,7 +76,9 @@ int cauchy_256_erasure_pattern(unsigned long long g, int k, int m, unsigned long
                                unsigned char *rows_out);
 
 /* Which kernels code (k, m, block_bytes): 1 = compile-time-scheduled (generated for this (k, m)),
- * 0 = the generic runtime-coefficient kernels, -1 = invalid parameters. Host only. */
+ * 2 = the runtime-coefficient tile kernels (any other (k, m) with block_bytes/8 >= 16),
+ * 0 = the generic per-column kernels (shorter blocks), -1 = invalid parameters, -2 = no GPU
+ * (the answer for shapes without generated kernels depends on where the code object loaded). */
 int cauchy_256_batch_path(int k, int m, int block_bytes);
 
 /* The library's private stream (used by the single-group calls) and a synchronize helper for

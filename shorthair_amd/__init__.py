@@ -14,7 +14,7 @@ import os
 
 __all__ = ["lib", "Block", "CAUCHY_256_VERSION", "cauchy_256_init", "cauchy_256_encode",
            "cauchy_256_decode", "encode_batch", "decode_batch", "decode_batch_out",
-           "fill_synthetic", "erasure_pattern", "batch_reserve", "batch_errors", "has_fixed", "default_stream", "sync", "LIB_PATH",
+           "fill_synthetic", "erasure_pattern", "batch_reserve", "batch_errors", "has_fixed", "path", "default_stream", "sync", "LIB_PATH",
            "EXPORTED_SYMBOLS"]
 
 CAUCHY_256_VERSION = 2
@@ -181,6 +181,13 @@ def batch_errors(stream=None):
 def has_fixed(k, m, block_bytes):
     """True when (k, m, block_bytes) runs on compile-time-scheduled kernels."""
     return lib.cauchy_256_batch_path(k, m, block_bytes) == 1
+
+
+def path(k, m, block_bytes):
+    """Kernel family that codes (k, m, block_bytes): "fixed" (compile-time schedules), "tile"
+    (runtime-coefficient snippet tiles), "generic" (per-column kernels, B/8 < 16) or "invalid"."""
+    rc = lib.cauchy_256_batch_path(k, m, block_bytes)
+    return {1: "fixed", 2: "tile", 0: "generic"}.get(rc, "invalid")
 
 
 def default_stream():

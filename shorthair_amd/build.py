@@ -12,7 +12,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, os.environ.get("SH_LIB_NAME", "libcauchy256.so"))
-SOURCES = ["kernels.hip", "stageb.hip", "fixed_dispatch.cpp", "cauchy_256_host.cpp", "shorthair_groups.cpp"]
+SOURCES = ["kernels.hip", "stageb.hip", "tile_snip.hip", "fixed_dispatch.cpp", "cauchy_256_host.cpp", "shorthair_groups.cpp"]
 HOST_SOURCES = ["gf256_host.cpp"]  # plain host C++ (no HIP): compiled with the host compiler
 CXX = os.environ.get("CXX", "g++")
 GEN_DIR = os.path.join(CSRC, os.environ.get("SH_GEN_DIR", "gen"))
@@ -53,20 +53,30 @@ FLAGS += os.environ.get("SH_EXTRA_FLAGS", "").split()  # experiments only (tools
 OBJ_DIR = os.path.join(HERE, os.environ.get("SH_OBJ_DIR", "build_obj"))
 
 
-def _headers():
-    """Every header a source can include: csrc/*.h*, the generated headers/.inc files, include/*.
-    (Conservative: any header change recompiles every object.)"""
-    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".hpp"))]
-    hs += [os.path.join(GEN_DIR, f) for f in os.listdir(GEN_DIR) if f.endswith((".h", ".inc"))]
-    inc = os.path.join(HERE, "..", "include")
-    hs += [os.path.join(inc, f) for f in os.listdir(inc)]
-    return hs
+def _includes(path, seen=None):
+    """Files `path` pulls in through #include "..." (recursively; resolved against the including
+    file's directory, csrc/ and the generated-kernel directory, as the -I flags do)."""
+    import re
+    seen = set() if seen is None else seen
+    try:
+        text = open(path, errors="replace").read()
+    except OSError:
+        return seen
+    for name in re.findall(r'^\s*#\s*include\s+"([^"]+)"', text, re.M):
+        for d in (os.path.dirname(path), CSRC, GEN_DIR):
+            cand = os.path.normpath(os.path.join(d, name))
+            if os.path.exists(cand):
+                if cand not in seen:
+                    seen.add(cand)
+                    _includes(cand, seen)
+                break
+    return seen
 
 
 def _compile(src, verbose):
     obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(
-            os.path.getmtime(src), *[os.path.getmtime(h) for h in _headers()]):
+            os.path.getmtime(src), *[os.path.getmtime(h) for h in _includes(src)], 0):
         return obj, None
     if os.path.basename(src) in HOST_SOURCES:
         cmd = [CXX, "-O3", "-std=c++17", "-fPIC", "-Wall", "-c", src, "-o", obj]

@@ -89,6 +89,13 @@ struct StreamState {
     int *d_errors = nullptr;
 };
 
+// One launch of the tile kernels: output rows [row0, row0 + nrows) with its snippet-address table.
+struct TileLaunch {
+    int row0, nrows, nsteps;
+    long long tstride;
+    uint32_t *targets;  // device [parts][tstride]
+};
+
 struct Context {
     std::mutex mu;          // guards lazy state (tables, caches, the stream map, profiling events)
     bool ready = false;
@@ -102,6 +109,8 @@ struct Context {
     // followed by the raw (m-1) x k rows 1..m-1 and the Cauchy parameters X'[k], Y'[m] for
     // decode setup.
     std::map<std::pair<int, int>, uint8_t *> gens;
+    // (k, m, dec) -> launches of the runtime-coefficient tile kernels (csrc/tile_snip.hip)
+    std::map<std::array<int, 3>, std::vector<TileLaunch>> tiles;
     // Decode state per stream: two decodes in flight on different streams never share scratch.
     std::map<hipStream_t, std::unique_ptr<StreamState>> streams;
     std::atomic<size_t> ws_reserve{0};  // cauchy_256_batch_reserve: minimum size of a workspace
@@ -229,6 +238,60 @@ uint8_t *generator(Context &c, int k, int m) {
     return d;
 }
 
+// Whether (k, m, B) can run on the runtime-coefficient tile kernels: fixed_geometry's 16-byte
+// chunks (B/8 >= 16) and a snippet table inside one 4 GB page (the kernels form the snippet
+// addresses from their low dwords).
+bool tile_usable(Context &c, int k, int m, int B) {
+    if (k < 2 || m < 2 || k + m > 256 || !sh::tile_ok(B)) return false;
+    if (std::getenv("SH_NO_TILE")) return false;  // measurement switch: the older generic kernels
+    const uint64_t lo = c.snip_base, hi = c.snip_base + static_cast<uint64_t>(sh::SNIP_NULL + 1) * sh::SNIP_STRIDE;
+    return (lo >> 32) == (hi >> 32);
+}
+
+// Measurement switch (never the default): SH_FORCE_TILE=1 routes shapes that have compile-time
+// kernels through the tile kernels too, to compare the two on the same shape.
+bool force_tile() {
+    static const bool f = std::getenv("SH_FORCE_TILE") != nullptr;
+    return f;
+}
+
+// Launch plan of the tile kernels for (k, m): <= 128 rows per launch; per launch and part-wave a
+// table of snippet-address low dwords, [step][8] per part (reference generator cauchy_matrix(),
+// cauchy_256.cpp:423-481, row 0 = ones). Decode (stage A): steps 0..k-1 are the received columns,
+// step k + i adds recovery row row0 + i into its residual row (coefficient 1 on that row only).
+const std::vector<TileLaunch> *tile_plan(Context &c, int k, int m, bool dec) {
+    std::lock_guard<std::mutex> g(c.mu);
+    auto it = c.tiles.find({k, m, dec ? 1 : 0});
+    if (it != c.tiles.end()) return &it->second;
+    const std::vector<uint8_t> G = sh::generator_matrix(k, m);  // [m][k], row 0 = ones
+    const uint32_t base = static_cast<uint32_t>(c.snip_base);
+    auto addr = [&](int cf) { return base + static_cast<uint32_t>(cf ? cf : sh::SNIP_NULL) * sh::SNIP_STRIDE; };
+    std::vector<TileLaunch> plan;
+    for (int row0 = 0; row0 < m; row0 += 128) {
+        TileLaunch L{};
+        L.row0 = row0;
+        L.nrows = std::min(128, m - row0);
+        L.nsteps = k + (dec ? L.nrows : 0);
+        const int parts = (L.nrows + 7) / 8;
+        const int S = sh::tile_steps_per_group(parts);
+        L.tstride = static_cast<long long>((L.nsteps + S - 1) / S) * S * 8;
+        std::vector<uint32_t> t(static_cast<size_t>(parts) * L.tstride, addr(0));
+        for (int p = 0; p < parts; ++p)
+            for (int x = 0; x < L.nsteps; ++x)
+                for (int j = 0; j < 8; ++j) {
+                    const int yy = 8 * p + j;
+                    if (yy >= L.nrows) continue;
+                    const int cf = x < k ? G[static_cast<size_t>(row0 + yy) * k + x] : (x - k == yy ? 1 : 0);
+                    t[static_cast<size_t>(p) * L.tstride + static_cast<size_t>(x) * 8 + j] = addr(cf);
+                }
+        if (hipMalloc(&L.targets, t.size() * sizeof(uint32_t)) != hipSuccess) return nullptr;
+        if (hipMemcpy(L.targets, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess)
+            return nullptr;
+        plan.push_back(L);
+    }
+    return &(c.tiles[{k, m, dec ? 1 : 0}] = std::move(plan));
+}
+
 // Batched calls take the caller's stream verbatim (NULL = the null stream, as in HIP itself).
 hipStream_t pick(void *stream) { return static_cast<hipStream_t>(stream); }
 
@@ -251,6 +314,37 @@ hipError_t launch_fixed_batch(int k, int m, int B, int groups, const uint8_t *in
     return sh::launch_fixed(k, m, a, dec, s);
 }
 
+// One pass of the tile kernels over the batch (encode, or decode stage A with position tables).
+int launch_tile_batch(Context &c, int k, int m, int B, int groups, const uint8_t *in, long long in_gs,
+                      uint8_t *out, long long out_gs, const uint8_t *pos, const uint8_t *rpos, bool dec,
+                      hipStream_t s) {
+    const std::vector<TileLaunch> *plan = tile_plan(c, k, m, dec);
+    if (!plan) return -2;
+    for (const TileLaunch &L : *plan) {
+        sh::TileArgs t{};
+        t.f.in = in;
+        t.f.in_gstride = in_gs;
+        t.f.in_bytes = static_cast<long long>(groups) * in_gs;
+        t.f.out = out + static_cast<long long>(L.row0) * B;
+        t.f.out_gstride = out_gs;
+        t.f.out_bytes = static_cast<long long>(groups) * out_gs - static_cast<long long>(L.row0) * B;
+        t.f.groups = groups;
+        t.f.geo = sh::fixed_geometry(B);
+        t.f.pos = pos;
+        t.f.rpos = rpos;
+        t.targets = L.targets;
+        t.tstride = L.tstride;
+        t.snip_hi = static_cast<uint32_t>(c.snip_base >> 32);
+        t.k = k;
+        t.m = m;
+        t.row0 = L.row0;
+        t.nrows = L.nrows;
+        t.nsteps = L.nsteps;
+        SH_CHECK(sh::launch_tile(t, dec, s));
+    }
+    return 0;
+}
+
 // ---- batched encode ----
 int encode_batch(int k, int m, int B, int groups, const uint8_t *d_in, uint8_t *d_out,
                  hipStream_t s) {
@@ -270,11 +364,13 @@ int encode_batch(int k, int m, int B, int groups, const uint8_t *d_in, uint8_t *
         SH_CHECK(sh::launch_xor_rows(d_in, in_gs, k, d_out, out_gs, B, groups, s));
         return (m == 1 || valid) ? 0 : -1;  // m == 1 returns before validation (:1503-1506)
     }
-    if (sh::has_fixed(k, m, B)) {
+    if (sh::has_fixed(k, m, B) && !force_tile()) {
         SH_CHECK(launch_fixed_batch(k, m, B, groups, d_in, in_gs, d_out, out_gs, nullptr, nullptr,
                                     false, s));
         return 0;
     }
+    if (tile_usable(c, k, m, B))
+        return launch_tile_batch(c, k, m, B, groups, d_in, in_gs, d_out, out_gs, nullptr, nullptr, false, s);
     uint8_t *gen = generator(c, k, m);
     if (!gen) return -2;
     sh::ApplyArgs a{};
@@ -311,7 +407,8 @@ struct DecodeWS {
 size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool need_recovered) {
     const sh::Geometry geo = sh::fixed_geometry(B);
     w.emax = std::min(k, m);
-    w.fixed = sh::has_fixed(k, m, B) && sh::stageb_fixed_ok(geo, w.emax);
+    // stage A over all m rows (compile-time or tile kernels), position tables, snippet stage B
+    w.fixed = (sh::has_fixed(k, m, B) || tile_usable(ctx(), k, m, B)) && sh::stageb_fixed_ok(geo, w.emax);
     w.small = w.fixed && sh::stageb_small_ok(geo, w.emax);
     w.ldA = w.fixed ? 0 : round4(k);
     w.ldB = (w.emax + 7) & ~7;  // stage-B coefficients [i][ldB] (transposed, 8-entry rows)
@@ -439,8 +536,13 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
     if (w.fixed) {
         // Stage A (compile-time generator, all m rows, erased columns read as zeros):
         //   residual_y = R_y + sum_{received x} M(C[y][x]) d_x
-        SH_CHECK(launch_fixed_batch(k, m, B, groups, d_blocks, static_cast<long long>(k) * B,
-                                      w.residual, static_cast<long long>(m) * B, w.pos, w.rpos, true, s));
+        if (sh::has_fixed(k, m, B) && !force_tile()) {
+            SH_CHECK(launch_fixed_batch(k, m, B, groups, d_blocks, static_cast<long long>(k) * B,
+                                        w.residual, static_cast<long long>(m) * B, w.pos, w.rpos, true, s));
+        } else if (int rc = launch_tile_batch(c, k, m, B, groups, d_blocks, static_cast<long long>(k) * B,
+                                              w.residual, static_cast<long long>(m) * B, w.pos, w.rpos, true, s)) {
+            return rc;
+        }
         if (ev) SH_CHECK(hipEventRecord(ev[2], s));
         // Stage B: recovered_j = sum_y M(S^-1[j][i(y)]) residual_y over the received rows y
         SH_CHECK(launch_stage_b(w, m, B, groups, dst, s));
@@ -662,7 +764,11 @@ extern "C" int cauchy_256_erasure_pattern(unsigned long long g, int k, int m, un
 
 extern "C" int cauchy_256_batch_path(int k, int m, int block_bytes) {
     if (k < 1 || m < 1 || k + m > 256 || block_bytes <= 0 || block_bytes % 8 != 0) return -1;
-    return sh::has_fixed(k, m, block_bytes) ? 1 : 0;
+    if (sh::has_fixed(k, m, block_bytes) && !force_tile()) return 1;
+    Context &c = ctx();
+    DeviceScope ds(c);
+    if (ds.rc) return ds.rc;
+    return tile_usable(c, k, m, block_bytes) ? 2 : 0;
 }
 
 extern "C" void *cauchy_256_default_stream(void) {

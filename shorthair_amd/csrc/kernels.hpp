@@ -172,6 +172,23 @@ struct FixedArgs {
     int groups_per_wg;        // set by the launcher
 };
 
+// Runtime-coefficient tile kernels (csrc/tile_snip.hip): every (k, m) with B % 8 == 0, B/8 >= 16.
+// One launch codes output rows [row0, row0 + nrows) (nrows <= 128) of every group: f.out points at
+// row row0 of group 0 (f.out_gstride = m * B). targets = per-part tables of snippet-address low
+// dwords, [parts][tstride] with tstride = ceil(nsteps / S) * S * 8 (S = tile_steps_per_group),
+// entry [p][x][j] for row 8p + j of the launch and step x (decode: x < k input column x,
+// x >= k recovery row row0 + x - k).
+struct TileArgs {
+    FixedArgs f;
+    const uint32_t *targets;
+    long long tstride;
+    uint32_t snip_hi;         // high dword of every snippet address
+    int k, m, row0, nrows, nsteps;
+};
+bool tile_ok(int B);
+int tile_steps_per_group(int parts);
+hipError_t launch_tile(const TileArgs &t, bool dec, hipStream_t stream);
+
 // Returns hipErrorNotSupported (and launches nothing) when (k, m) has no generated kernel or the
 // block is too short (sub < 4).
 hipError_t launch_fixed(int k, int m, FixedArgs a, bool dec, hipStream_t stream);

@@ -216,6 +216,41 @@ def test_decode_batch_roundtrip_and_oracle(sh, k, m, B, G, e_fixed):
         assert np.array_equal(np.stack(b), blocks[g].cpu().numpy())
 
 
+# Off-grid (k, m): the runtime-coefficient tile kernels (csrc/tile_snip.hip) -- one part (m <= 8),
+# 2..8 parts (two column-waves), 9..16 parts (one column-wave), two launches (m > 128), the
+# shapes Shorthair's policy issues between the compiled pairs, and odd group counts (partial tiles).
+TILE_SHAPES = [(120, 136, 1400, 37), (150, 40, 1400, 301), (50, 10, 1000, 513), (180, 76, 1352, 45),
+               (2, 254, 128, 61), (100, 100, 200, 77), (5, 3, 128, 999), (70, 72, 520, 130),
+               (17, 5, 1352, 9), (60, 24, 4104, 11), (33, 33, 136, 257), (240, 16, 264, 40)]
+
+
+@pytest.mark.parametrize("k,m,B,G", TILE_SHAPES)
+def test_tile_encode_decode_vs_oracle(sh, k, m, B, G):
+    """Encode and decode of shapes without compile-time kernels run on the tile kernels (path 2):
+    encode bit-exact against the oracle on sampled groups; decode (random e up to min(k, m))
+    recovers every group of the batch and matches the oracle's decode on sampled groups."""
+    import torch
+    assert sh.path(k, m, B) == "tile"
+    cfg = 0x7E + k + m
+    data, rec, blocks, d_rows, rows, es = _decode_inputs(k, m, B, G, cfg, 0)
+    sample = sorted({0, G // 2, G - 1})
+    exp = _oracle_encode_groups(k, m, B, cfg, sample)
+    for g in sample:
+        assert np.array_equal(rec[g].cpu().numpy(), exp[g][1]), f"encode g={g}"
+    orig = blocks.clone()
+    assert sh.decode_batch(k, m, B, G, blocks, d_rows) == 0
+    _sync()
+    new_rows = d_rows.cpu().numpy()
+    truth = data[torch.arange(G, device="cuda")[:, None], torch.from_numpy(new_rows).cuda().long()]
+    assert torch.equal(blocks, truth), "round trip"
+    ora = po.oracle()
+    for g in sample:
+        b = [x.copy() for x in orig[g].cpu().numpy()]
+        rc, nr = ora.decode(k, m, b, list(rows[g]), B)
+        assert rc == 0 and nr == new_rows[g].tolist()
+        assert np.array_equal(np.stack(b), blocks[g].cpu().numpy()), g
+
+
 def test_decode_batch_out_matches_inplace(sh):
     import torch
     k, m, B, G = 200, 32, 1400, 512

@@ -134,6 +134,16 @@ def main():
             enc_case(f"big_enc_c4_{k}_{m}_{B}", 5000 + k + B, k, m, B, full=False)
             dec_case(f"big_dec_c4_{k}_{m}_{B}", 6000 + k + B, k, m, B, 0, full=False)
 
+    # ---- off-grid shapes (no compile-time kernels: the runtime-coefficient tile kernels code
+    # them): what Shorthair's policy issues between the compiled pairs (k = packets queued in the
+    # interval, m = R clamped to 256 - k, Shorthair.cpp:1130-1174, :502-504), plus the edges of
+    # the tile kernels (one part, 16 parts, two launches for m > 128, short sub-blocks).
+    for i, (k, m, B, e) in enumerate([(120, 136, 1400, 64), (150, 40, 1400, 40), (50, 10, 1000, 7),
+                                      (180, 76, 1352, 33), (2, 254, 128, 2), (100, 100, 200, 0),
+                                      (5, 3, 128, 3), (70, 72, 520, 0)]):
+        enc_case(f"offgrid_enc_{k}_{m}_{B}", 7000 + i, k, m, B, full=False)
+        dec_case(f"offgrid_dec_{k}_{m}_{B}_e{e or 'r'}", 7100 + i, k, m, B, e, order="shuffled", full=False)
+
     np.savez_compressed(os.path.join(OUT, "golden_small.npz"), **arrays)
     with open(os.path.join(OUT, "manifest.json"), "w") as f:
         json.dump(dict(generator="tools/gen_golden.py", source="oracle/_ref/libref_cauchy.so "
