@@ -397,12 +397,20 @@ int encode_batch(int k, int m, int B, int groups, const uint8_t *d_in, uint8_t *
 struct DecodeWS {
     bool fixed;       // stage A by a compile-time-scheduled kernel, stage B by stageb_fixed
     bool small;       // ... and stage B by stageb_small (nq <= 16 word columns: byte coefficients)
+    bool v2;          // ... or by stageb_v2 (byte coefficients, one workgroup per group chunk)
     int emax, ldA, ldB, nres;  // nres: residual rows per group (m when fixed, else emax)
     int *e;
     uint8_t *rec_idx, *erasures, *coefA, *coefB, *residual, *recovered, *pos, *rpos, *rrow;
     uint64_t *targets;
     long long coefA_gs, coefB_gs;
 };
+
+// Stage B after a full-residual stage A: stageb_v2 unless SH_STAGEB_OLD is set (measurement switch:
+// round 2's stageb_fixed / stageb_regs with setup-written snippet addresses).
+bool stageb_v2_on(const sh::Geometry &geo, int emax) {
+    static const bool old = std::getenv("SH_STAGEB_OLD") != nullptr;
+    return !old && sh::stageb_v2_ok(geo, emax);
+}
 
 size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool need_recovered) {
     const sh::Geometry geo = sh::fixed_geometry(B);
@@ -426,9 +434,11 @@ size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool n
     w.rec_idx = take(G * w.emax);
     w.erasures = take(G * w.emax);
     w.coefA = w.fixed ? nullptr : take(G * w.coefA_gs);
-    w.coefB = (w.fixed && !w.small) ? nullptr : take(G * w.coefB_gs);
-    w.targets = (w.fixed && !w.small) ? reinterpret_cast<uint64_t *>(take(G * w.emax * w.ldB * sizeof(uint64_t)))
-                                      : nullptr;
+    w.coefB = (w.fixed && !w.small && !stageb_v2_on(geo, w.emax)) ? nullptr : take(G * w.coefB_gs);
+    w.v2 = w.fixed && !w.small && stageb_v2_on(geo, w.emax);
+    w.targets = (w.fixed && !w.small && !w.v2)
+                    ? reinterpret_cast<uint64_t *>(take(G * w.emax * w.ldB * sizeof(uint64_t)))
+                    : nullptr;
     w.rrow = w.fixed ? take(G * round4(w.emax)) : nullptr;
     w.pos = w.fixed ? take(G * round4(k)) : nullptr;
     w.rpos = w.fixed ? take(G * round4(m)) : nullptr;
@@ -454,6 +464,24 @@ hipError_t launch_stage_b(const DecodeWS &w, int n_in, int B, int groups, uint8_
         f.groups = groups;
         f.geo = sh::fixed_geometry(B);
         return sh::launch_stageb_small(f, s);
+    }
+    if (w.v2) {
+        sh::StageBV2Args f{};
+        f.in = w.residual;
+        f.in_gstride = static_cast<long long>(n_in) * B;
+        f.out = dst;
+        f.out_gstride = static_cast<long long>(w.emax) * B;
+        f.e = w.e;
+        f.rrow = w.rrow;
+        f.ldR = round4(w.emax);
+        f.coefT = w.coefB;
+        f.coefT_gstride = w.coefB_gs;
+        f.ldT = w.ldB;
+        f.emax = w.emax;
+        f.groups = groups;
+        f.geo = sh::fixed_geometry(B);
+        f.snip_base = ctx().snip_base;
+        return sh::launch_stageb_v2(f, s);
     }
     if (w.fixed) {
         sh::StageBFixedArgs f{};

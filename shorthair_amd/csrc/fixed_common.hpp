@@ -44,7 +44,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "kernels.hpp"
+#include "geometry.hpp"
 
 namespace sh {
 namespace fixed {

@@ -5,36 +5,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "geometry.hpp"
+
 namespace sh {
-
-// Column geometry of a block size B (multiple of 8): sub = B/8 bytes per sub-block, nq 32-bit
-// word columns per sub-block, the last one holding `tail` (1..4) valid bytes.
-struct Geometry {
-    int B;
-    int sub;
-    int nq;
-    int tail;
-};
-
-inline Geometry make_geometry(int B) {
-    Geometry g;
-    g.B = B;
-    g.sub = B / 8;
-    g.nq = (g.sub + 3) / 4;
-    g.tail = g.sub - 4 * (g.nq - 1);
-    return g;
-}
-
-// Geometry of the compile-time path: the word columns per sub-block are rounded up to a multiple
-// of 4 so 16-byte (4-column) chunks never straddle two groups; the last chunk of a sub-block is
-// shifted back by 4 * nq - sub (< 16) bytes so it ends at the sub-block's end (its first bytes
-// are computed twice, identically). Needs sub >= 16.
-inline Geometry fixed_geometry(int B) {
-    Geometry g = make_geometry(B);
-    g.nq = (g.nq + 3) & ~3;
-    g.tail = 4;
-    return g;
-}
 
 struct ApplyArgs {
     const uint8_t *in;
@@ -133,6 +106,26 @@ struct StageBFixedArgs {
 };
 bool stageb_fixed_ok(const Geometry &geo, int emax);
 hipError_t launch_stageb_fixed(const StageBFixedArgs &a, hipStream_t stream);
+// Decode stage B after a full-residual stage A (compile-time or tile kernels), byte coefficients:
+// out[g][j] = sum_{i < e} M(coefT[g][i][j]) in[g][rrow[g][i]] (csrc/stageb.hip, stageb_v2).
+struct StageBV2Args {
+    const uint8_t *in;        // [G][n_in][B] residual rows (all m generator rows)
+    long long in_gstride;
+    uint8_t *out;             // [G][emax][B]
+    long long out_gstride;
+    const int *e;             // [G] received recovery blocks = outputs (<= 0: nothing to do)
+    const uint8_t *rrow;      // [G][ldR] residual row of the i-th received recovery block
+    int ldR;                  // round4(emax)
+    const uint8_t *coefT;     // [G][emax][ldT]: entry [i][j] = S^-1[j][i] (0 past e)
+    long long coefT_gstride;
+    int ldT;                  // multiple of 8
+    int emax;
+    int groups;
+    Geometry geo;
+    uint64_t snip_base;       // address of snippet 0 of the accumulating table (stride SNIP_STRIDE)
+};
+bool stageb_v2_ok(const Geometry &geo, int emax);
+hipError_t launch_stageb_v2(const StageBV2Args &a, hipStream_t stream);
 // Decode stage B for small blocks after a compile-time stage A (csrc/stageb.hip, stageb_small):
 // per-lane coefficients, so one wave serves 64 / nq groups.
 struct StageBSmallArgs {
@@ -156,21 +149,6 @@ hipError_t launch_stageb_small(const StageBSmallArgs &a, hipStream_t stream);
 hipError_t stageb_snip_base(uint64_t *out_host, hipStream_t stream);
 constexpr int SNIP_STRIDE = 72;   // bytes per stage-B snippet (gen_fixed_kernels.py)
 constexpr int SNIP_NULL = 256;    // index of the null snippet
-
-// Compile-time-scheduled kernels (csrc/gen/, tools/gen_fixed_kernels.py).
-struct FixedArgs {
-    const uint8_t *in;        // encode: data [G][k][B]; decode A: received blocks [G][k][B]
-    long long in_gstride;
-    long long in_bytes;       // groups * in_gstride
-    uint8_t *out;             // encode: recovery [G][m][B]; decode A: residual [G][m][B]
-    long long out_gstride;
-    long long out_bytes;      // groups * out_gstride
-    int groups;
-    Geometry geo;
-    const uint8_t *pos;       // decode: [G][round4(k)] array index of original row x, 0xFF = erased
-    const uint8_t *rpos;      // decode: [G][round4(m)] array index of recovery row y, 0xFF = absent
-    int groups_per_wg;        // set by the launcher
-};
 
 // Runtime-coefficient tile kernels (csrc/tile_snip.hip): every (k, m) with B % 8 == 0, B/8 >= 16.
 // One launch codes output rows [row0, row0 + nrows) (nrows <= 128) of every group: f.out points at

@@ -435,6 +435,227 @@ __global__ __launch_bounds__(256, 4) void stageb_fixed(StageBFixedArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// stageb_v2: one workgroup = one group x one 64-column chunk x up to 8*NW outputs (NW waves of 8),
+// so for e <= 8*NW every residual row is fetched ONCE per (group, chunk) however large e is
+// (stageb_fixed re-streamed all e rows per 32 outputs: e = 56..66 at the Tester's shapes).
+// Per row a wave needs the snippet addresses of its 8 coefficients S^-1[j0..j0+7][i]; they come
+// from the byte coefficients (setup's transposed [i][j] table), copied once per workgroup into
+// LDS ([wave][row], 8 bytes each), read one row ahead with the row's words (one ds_read_b64 at a
+// wave-uniform address, two v_readfirstlane) and turned into addresses base + 72*c by SALU. The
+// rows' scalar loads of round 2 (one 64-byte s_load of addresses per row, first touch of
+// 64 MB written by the setup) exposed a memory latency on every row.
+// ---------------------------------------------------------------------------------------------
+#define SH_V2_STEP_ASM                                                                            \
+    "v_mov_b32 v97, %[d0]\n"                                                                      \
+    "v_mov_b32 v98, %[d1]\n"                                                                      \
+    "v_mov_b32 v100, %[d2]\n"                                                                     \
+    "v_mov_b32 v104, %[d3]\n"                                                                     \
+    "v_mov_b32 v113, %[d4]\n"                                                                     \
+    "v_mov_b32 v114, %[d5]\n"                                                                     \
+    "v_mov_b32 v116, %[d6]\n"                                                                     \
+    "v_mov_b32 v120, %[d7]\n"                                                                     \
+    "v_xor_b32 v99, %[d0], %[d1]\n"                                                               \
+    "v_xor_b32 v115, %[d4], %[d5]\n"                                                              \
+    "v_xor_b32 v101, %[d0], %[d2]\n"                                                              \
+    "v_xor_b32 v117, %[d4], %[d6]\n"                                                              \
+    "v_xor_b32 v102, %[d1], %[d2]\n"                                                              \
+    "v_xor_b32 v118, %[d5], %[d6]\n"                                                              \
+    "v_xor_b32 v105, %[d0], %[d3]\n"                                                              \
+    "v_xor_b32 v121, %[d4], %[d7]\n"                                                              \
+    "v_xor_b32 v106, %[d1], %[d3]\n"                                                              \
+    "v_xor_b32 v122, %[d5], %[d7]\n"                                                              \
+    "v_xor_b32 v108, %[d2], %[d3]\n"                                                              \
+    "v_xor_b32 v124, %[d6], %[d7]\n"                                                              \
+    "v_xor_b32 v103, v99, %[d2]\n"                                                                \
+    "v_xor_b32 v119, v115, %[d6]\n"                                                               \
+    "v_xor_b32 v107, v99, %[d3]\n"                                                                \
+    "v_xor_b32 v123, v115, %[d7]\n"                                                               \
+    "v_xor_b32 v109, v101, %[d3]\n"                                                               \
+    "v_xor_b32 v125, v117, %[d7]\n"                                                               \
+    "v_xor_b32 v110, v102, %[d3]\n"                                                               \
+    "v_xor_b32 v126, v118, %[d7]\n"                                                               \
+    "v_xor_b32 v111, v103, %[d3]\n"                                                               \
+    "v_xor_b32 v127, v119, %[d7]\n"                                                               \
+    "s_mov_b32 s43, %[hi]\n"                                                                      \
+    "s_bfe_u32 s42, %[c0], 0x80000\n"                                                             \
+    "s_lshl3_add_u32 s42, s42, s42\n"                                                             \
+    "s_lshl3_add_u32 s42, s42, %[lo]\n"                                                           \
+    "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"                                                     \
+    "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
+    "s_bfe_u32 s42, %[c0], 0x80008\n"                                                             \
+    "s_lshl3_add_u32 s42, s42, s42\n"                                                             \
+    "s_lshl3_add_u32 s42, s42, %[lo]\n"                                                           \
+    "s_set_gpr_idx_idx 8\n"                                                                       \
+    "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
+    "s_bfe_u32 s42, %[c0], 0x80010\n"                                                             \
+    "s_lshl3_add_u32 s42, s42, s42\n"                                                             \
+    "s_lshl3_add_u32 s42, s42, %[lo]\n"                                                           \
+    "s_set_gpr_idx_idx 16\n"                                                                      \
+    "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
+    "s_lshr_b32 s42, %[c0], 24\n"                                                                 \
+    "s_lshl3_add_u32 s42, s42, s42\n"                                                             \
+    "s_lshl3_add_u32 s42, s42, %[lo]\n"                                                           \
+    "s_set_gpr_idx_idx 24\n"                                                                      \
+    "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
+    "s_bfe_u32 s42, %[c1], 0x80000\n"                                                             \
+    "s_lshl3_add_u32 s42, s42, s42\n"                                                             \
+    "s_lshl3_add_u32 s42, s42, %[lo]\n"                                                           \
+    "s_set_gpr_idx_idx 32\n"                                                                      \
+    "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
+    "s_bfe_u32 s42, %[c1], 0x80008\n"                                                             \
+    "s_lshl3_add_u32 s42, s42, s42\n"                                                             \
+    "s_lshl3_add_u32 s42, s42, %[lo]\n"                                                           \
+    "s_set_gpr_idx_idx 40\n"                                                                      \
+    "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
+    "s_bfe_u32 s42, %[c1], 0x80010\n"                                                             \
+    "s_lshl3_add_u32 s42, s42, s42\n"                                                             \
+    "s_lshl3_add_u32 s42, s42, %[lo]\n"                                                           \
+    "s_set_gpr_idx_idx 48\n"                                                                      \
+    "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
+    "s_lshr_b32 s42, %[c1], 24\n"                                                                 \
+    "s_lshl3_add_u32 s42, s42, s42\n"                                                             \
+    "s_lshl3_add_u32 s42, s42, %[lo]\n"                                                           \
+    "s_set_gpr_idx_idx 56\n"                                                                      \
+    "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
+    "s_set_gpr_idx_off"
+
+// acc sets j += M(c_j) * d, c_j = byte j of (c0, c1) (a zero byte runs snippet 0: XORs of zeros)
+__device__ __forceinline__ void v2_row(const Row8 &d, uint32_t c0, uint32_t c1, uint32_t lo, uint32_t hi,
+                                       u32x16 &a01, u32x16 &a23, u32x16 &a45, u32x16 &a67, uint32_t &z0,
+                                       uint32_t &z1) {
+    asm volatile(SH_V2_STEP_ASM
+                 : "+{v[32:47]}"(a01), "+{v[48:63]}"(a23), "+{v[64:79]}"(a45), "+{v[80:95]}"(a67),
+                   "+{v96}"(z0), "+{v112}"(z1)
+                 : [d0] "v"(d.w[0]), [d1] "v"(d.w[1]), [d2] "v"(d.w[2]), [d3] "v"(d.w[3]), [d4] "v"(d.w[4]),
+                   [d5] "v"(d.w[5]), [d6] "v"(d.w[6]), [d7] "v"(d.w[7]), [c0] "s"(c0), [c1] "s"(c1),
+                   [lo] "s"(lo), [hi] "s"(hi)
+                 : "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107",
+                   "v108", "v109", "v110", "v111", "v113", "v114", "v115", "v116", "v117", "v118", "v119",
+                   "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "s40", "s41", "s42",
+                   "s43", "m0", "scc", "memory");
+}
+
+constexpr int V2_MAXE = 128;  // emax = min(k, m) <= 128 whenever k + m <= 256
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void stageb_v2(StageBV2Args a) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[RB_R * RB_ROW];
+    __shared__ __attribute__((aligned(8))) uint32_t cf[NW][V2_MAXE][2];  // [wave][row] coefficient bytes
+    const Geometry geo = a.geo;
+    const int ncc = (geo.nq + 63) / 64;
+    const int g = blockIdx.x / ncc;
+    const int cc = blockIdx.x - g * ncc;
+    const int c0 = cc * 64;
+    const int ncols = min(64, geo.nq - c0);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int e = a.e[g];
+    if (e <= 0) return;  // uniform over the workgroup
+    const int j0 = (blockIdx.y * NW + wave) * 8;
+    const bool active = j0 < e;
+    // this wave's coefficient bytes S^-1[j0..j0+7][i], i < e (transposed table [i][j]: 8
+    // contiguous bytes per row), into LDS; rows 2l and 2l+1 per lane
+    const uint8_t *cg = a.coefT + static_cast<long long>(g) * a.coefT_gstride + j0;
+    for (int i = lane; i < 2 * e && active; i += 64) {
+        uint32_t w;
+        __builtin_memcpy(&w, cg + static_cast<long long>(i >> 1) * a.ldT + 4 * (i & 1), 4);
+        cf[wave][i >> 1][i & 1] = w;
+    }
+    // the group's compacted residual-row list, 4 rows per lane (readlane by the issuing waves)
+    uint32_t rrv = 0;
+    if (4 * lane < e) __builtin_memcpy(&rrv, a.rrow + static_cast<long long>(g) * a.ldR + 4 * lane, 4);
+    const long long gbase = static_cast<long long>(g) * a.in_gstride;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.in + gbase), static_cast<short>(0), static_cast<int>(a.in_gstride), 0x00020000);
+    const int off = wave * 1024 + lane * 16;
+    const int sa = off / 256, cq = (off % 256) / 4;
+    const uint32_t dsrc = (c0 + cq < geo.nq) ? colx_off(c0 + cq, geo.nq, geo.sub) + static_cast<uint32_t>(sa * geo.sub)
+                                             : 0x80000000u;
+    const int elast = e - 1;
+    auto issue = [&](int i) {
+        if (wave < 2) {
+            const int x = min(i, elast);
+            const uint32_t w = __builtin_amdgcn_readlane(rrv, x >> 2);
+            const uint32_t soff = ((w >> (8 * (x & 3))) & 0xFFu) * static_cast<uint32_t>(geo.B);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(ring + (i % RB_R) * RB_ROW + wave * 1024),
+                                                     16, i < e ? dsrc : 0x80000000u, soff, 0, 0);
+        }
+    };
+    u32x16 a01, a23, a45, a67;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) a01[t] = a23[t] = a45[t] = a67[t] = 0;
+    uint32_t z0 = 0, z1 = 0;
+    const uint32_t lo = static_cast<uint32_t>(a.snip_base), hi = static_cast<uint32_t>(a.snip_base >> 32);
+    for (int i = 0; i < RB_R - RB_S; ++i) issue(i);
+    const int ngroups = (e + RB_S - 1) / RB_S;
+    for (int ig = 0; ig < ngroups; ++ig) {
+        // own DMAs of rows 4ig..4ig+3 landed (RB_R - 2 * RB_S younger ones may be outstanding);
+        // the first barrier also publishes the coefficient copies
+        if (wave < 2)
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(RB_R - 2 * RB_S) : "memory");
+        else
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+        for (int r = 0; r < RB_S; ++r) issue(ig * RB_S + RB_R - RB_S + r);
+        if (!active) continue;
+#pragma unroll
+        for (int r = 0; r < RB_S; ++r) {
+            const int i = ig * RB_S + r;
+            if (i >= e) break;  // uniform
+            const uint8_t *slot = ring + (i % RB_R) * RB_ROW + lane * 4;
+            Row8 d;
+#pragma unroll
+            for (int s = 0; s < 8; ++s) d.w[s] = *reinterpret_cast<const uint32_t *>(slot + s * 256);
+            const uint32_t q0 = __builtin_amdgcn_readfirstlane(cf[wave][i][0]);
+            const uint32_t q1 = __builtin_amdgcn_readfirstlane(cf[wave][i][1]);
+            v2_row(d, q0, q1, lo, hi, a01, a23, a45, a67, z0, z1);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no ring DMA may land after the workgroup ends
+    if (!active || lane >= ncols) return;
+    uint32_t acc[8][8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        acc[0][b] = a01[b]; acc[1][b] = a01[8 + b];
+        acc[2][b] = a23[b]; acc[3][b] = a23[8 + b];
+        acc[4][b] = a45[b]; acc[5][b] = a45[8 + b];
+        acc[6][b] = a67[b]; acc[7][b] = a67[8 + b];
+    }
+    uint8_t *out = a.out + static_cast<long long>(g) * a.out_gstride + colx_off(c0 + lane, geo.nq, geo.sub);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (j0 + j >= e) break;
+        uint8_t *row = out + static_cast<long long>(j0 + j) * geo.B;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) __builtin_memcpy(row + b * geo.sub, &acc[j][b], 4);
+    }
+}
+
+bool stageb_v2_ok(const Geometry &geo, int emax) {
+    return geo.nq % 4 == 0 && geo.sub >= 16 && emax >= 1 && emax <= V2_MAXE;
+}
+
+hipError_t launch_stageb_v2(const StageBV2Args &a, hipStream_t stream) {
+    if (a.groups <= 0 || a.emax <= 0) return hipSuccess;
+    if (!stageb_v2_ok(a.geo, a.emax)) return hipErrorNotSupported;
+    const int ncc = (a.geo.nq + 63) / 64;
+    const int octets = (a.emax + 7) / 8;
+    // Output chunks of <= 8 waves (64 outputs) per workgroup, as few as possible (each chunk
+    // streams all e rows), split evenly: 4..8 waves (4 waves per SIMD at 128 VGPRs).
+    const int chunks = (octets + 7) / 8;
+    const int nw = std::max(4, (octets + chunks - 1) / chunks);
+    dim3 grid(static_cast<unsigned>(ncc) * a.groups, (octets + nw - 1) / nw, 1);
+    switch (nw) {
+        case 4: hipLaunchKernelGGL(stageb_v2<4>, grid, dim3(256), 0, stream, a); break;
+        case 5: hipLaunchKernelGGL(stageb_v2<5>, grid, dim3(320), 0, stream, a); break;
+        case 6: hipLaunchKernelGGL(stageb_v2<6>, grid, dim3(384), 0, stream, a); break;
+        case 7: hipLaunchKernelGGL(stageb_v2<7>, grid, dim3(448), 0, stream, a); break;
+        default: hipLaunchKernelGGL(stageb_v2<8>, grid, dim3(512), 0, stream, a); break;
+    }
+    return hipGetLastError();
+}
+
 // Decode stage B for small blocks (fixed geometry with nq <= 16 word columns, B <= 512). A
 // group fills only nq lanes there, and a snippet's coefficient is wave-uniform, so stageb_fixed
 // would leave 64 - nq lanes idle; here each lane applies its own group's coefficients instead and

@@ -38,7 +38,8 @@ READ_PIN = os.environ.get("SH_READ_PIN", "0") == "1"
 # Measurement-only ablations for A/B libraries built by tools/build_variant.sh (never the product
 # default, results are wrong), comma-separated: "nodma" = no input DMA (compute on whatever the
 # ring holds), "novalu" = DMA, ring reads, barriers and stores but no XOR work, "nobar" = no
-# vmcnt wait / barrier (only meaningful with nodma), "nostore" = no output stores.
+# vmcnt wait / barrier (only meaningful with nodma), "nostore" = no output stores, "samecode" =
+# every part-wave runs part 0's body (one instruction stream per workgroup instead of P).
 ABLATE = set(filter(None, os.environ.get("SH_GEN_ABLATE", "").split(",")))
 
 
@@ -298,7 +299,11 @@ def gen_config(k, m):
             out.append("")
         out.append(f"template <class Src, class Snk>")
         out.append(f"__device__ __forceinline__ void run_{name}_{mode}(int part, const Src &src, const Snk &sink) {{")
+        if "samecode" in ABLATE:  # timing only: every part-wave runs part 0's code (one code stream)
+            out.append(f"    run_{name}_{mode}_p0(src, sink);")
         for p in range(len(parts)):
+            if "samecode" in ABLATE:
+                break
             kw = "if" if p == 0 else "else if"
             out.append(f"    {kw} (part == {p}) run_{name}_{mode}_p{p}(src, sink);")
         out.append("}")
