@@ -571,7 +571,7 @@ def main():
         dom = (("encode kernel", enc_ms) if not (a_ms > enc_ms) else ("decode stage-A kernel", a_ms))
         pmc, traffic_src = pmc_traffic(sh, k, m, B, G, args.erasures)
         names = {"encode": f"sh::fixed::kern_k{k}_m{m}_enc", "decode_stageA": f"sh::fixed::kern_k{k}_m{m}_dec",
-                 "decode_stageB": "sh::stageb_fixed"}
+                 "decode_stageB": "sh::stageb_v2"}
         e_all = int(es.sum())
         # stage A reads the k received blocks (survivors + recovery rows) and writes m residual
         # rows, like encode; stage B reads e residual rows and writes e recovered blocks
@@ -580,13 +580,15 @@ def main():
         pmc_line = None
         if pmc:
             pmc_line = {}
+            def find(nm):  # rocprofv3 names templates as "void sh::stageb_v2<4>(sh::StageBV2Args)"
+                return next((v for key, v in pmc.items() if key == nm or key.split("(")[0].split(" ")[-1].split("<")[0] == nm), None)
             for op, nm in names.items():
-                if nm in pmc:
-                    t = pmc[nm]
+                t = find(nm)
+                if t is not None:
                     pmc_line[op] = {"read_bytes": t["read_bytes"], "write_bytes": t["write_bytes"],
                                     "alg_bytes": alg[op], "traffic_over_alg": round(t["hbm_bytes"] / alg[op], 3)}
             dom_op = "encode" if dom[0].startswith("encode") else "decode_stageA"
-            traffic = pmc.get(names[dom_op], {}).get("hbm_bytes")
+            traffic = (find(names[dom_op]) or {}).get("hbm_bytes")
         threads = args.cpu_threads or host_cores()
         cpu = None if args.no_cpu else cpu_baseline(k, m, B, args.erasures, args.cpu_seconds, threads)
         line = {

@@ -405,11 +405,14 @@ struct DecodeWS {
     long long coefA_gs, coefB_gs;
 };
 
-// Stage B after a full-residual stage A: stageb_v2 unless SH_STAGEB_OLD is set (measurement switch:
-// round 2's stageb_fixed / stageb_regs with setup-written snippet addresses).
+// Stage B after a full-residual stage A: stageb_v2 for 16 < emax <= 64, where it measured faster
+// ((200,32) e = 32: 0.34 vs 0.39 ms; (200,56) e = 56: 0.667 vs 0.741 ms); round 2's kernels with
+// setup-written snippet addresses elsewhere: stageb_regs for emax <= 16 (C2 decode 0.72 vs 0.79 ms,
+// (28,4,1400) 0.51 vs 0.66 ms) and stageb_fixed above 64 ((190,66) decode 2.57 vs 2.89 ms).
+// SH_STAGEB_OLD=1 (measurement switch) selects round 2's kernels everywhere.
 bool stageb_v2_on(const sh::Geometry &geo, int emax) {
     static const bool old = std::getenv("SH_STAGEB_OLD") != nullptr;
-    return !old && sh::stageb_v2_ok(geo, emax);
+    return !old && emax > 16 && emax <= 64 && sh::stageb_v2_ok(geo, emax);
 }
 
 size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool need_recovered) {
@@ -686,14 +689,12 @@ extern "C" int cauchy_256_decode_batch_out(int k, int m, int block_bytes, int gr
     WsLease ls;
     if (int rc = lease_workspace(c, s, carve(w, nullptr, k, m, block_bytes, groups, false), ls)) return rc;
     carve(w, ls.p, k, m, block_bytes, groups, false);
-    if (int rc = decode_core(c, k, m, block_bytes, groups, static_cast<const uint8_t *>(d_blocks),
-                             d_rows, w, ls.errors, static_cast<uint8_t *>(d_out), s))
-        return rc;
-    SH_CHECK(hipMemcpyAsync(d_out_rows, w.erasures, static_cast<size_t>(groups) * w.emax,
-                            hipMemcpyDeviceToDevice, s));
-    SH_CHECK(hipMemcpyAsync(d_out_count, w.e, static_cast<size_t>(groups) * sizeof(int),
-                            hipMemcpyDeviceToDevice, s));
-    return 0;
+    // the setup writes the erasure list ([G][emax]) and the counts ([G]) straight into the
+    // caller's outputs (same layouts as the workspace's): no copies after the decode
+    w.erasures = d_out_rows;
+    w.e = d_out_count;
+    return decode_core(c, k, m, block_bytes, groups, static_cast<const uint8_t *>(d_blocks), d_rows, w,
+                       ls.errors, static_cast<uint8_t *>(d_out), s);
 }
 
 extern "C" int cauchy_256_batch_reserve(int k, int m, int block_bytes, int groups) {

@@ -1,6 +1,4 @@
 mkdir -p gpurun_out
-for b in 4 2 8 1; do timeout -k 10 60 tools/jump_probe $b 4000 || exit 1; done
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q -k "decode or tile or golden" --timeout 200 --timeout-method thread > gpurun_out/t5.log 2>&1; rc=$?; tail -3 gpurun_out/t5.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 120 python tools/run_ops.py --op both --iters 10 2>&1 | grep -v amdgpu.ids || exit 1
-timeout -k 10 120 python tools/run_ops.py --op decode --iters 5 --k 200 --m 56 --block 1352 --groups 5547 --erasures 56 2>&1 | grep -v amdgpu.ids || exit 1
-timeout -k 10 120 python tools/run_ops.py --op decode --iters 5 --k 190 --m 66 --block 1336 --groups 5909 --erasures 66 2>&1 | grep -v amdgpu.ids || exit 1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?; tail -3 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
+IFETCH="SQC_ICACHE_REQ SQC_ICACHE_MISSES SQC_TC_INST_REQ SQC_ICACHE_BUSY_CYCLES" timeout -k 10 900 bash tools/gpu_profile.sh a > gpurun_out/prof_a.log 2>&1; rc=$?; tail -25 gpurun_out/prof_a.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 500 python bench.py > gpurun_out/bench_a.json 2> gpurun_out/bench_a.err; rc=$?; tail -c 600 gpurun_out/bench_a.json; exit $rc

@@ -44,7 +44,25 @@ COEF = [0x53, 0xCA, 0x1F, 0x8E, 0x35, 0xB2, 0x67, 0xD9]
 
 def body(mode):
     L = []
-    if mode == "inline":
+    if mode == "noidx":  # absolute registers, no VGPR-index mode
+        for j, c in enumerate(COEF):
+            v = c
+            for b in range(8):
+                L.append(f"v_bitop3_b32 v{ACC + 8 * j + b}, v{ACC + 8 * j + b}, v{T0 + (v & 15)}, v{T1 + (v >> 4)} bitop3:0x96")
+                v = gmul2(v)
+    elif mode == "idx0":  # VGPR-index mode on, M0 never changed inside
+        L.append("s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)")
+        for j, c in enumerate(COEF):
+            L += snippet(c, [])
+        L.append("s_set_gpr_idx_off")
+    elif mode == "idxnop":  # as inline, with s_nop 1 after each index change
+        L.append("s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)")
+        for j, c in enumerate(COEF):
+            if j:
+                L.append(f"s_set_gpr_idx_idx {8 * j}")
+            L += snippet(c, [])
+        L.append("s_set_gpr_idx_off")
+    elif mode == "inline":
         L.append("s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)")
         for j, c in enumerate(COEF):
             if j:
@@ -61,6 +79,21 @@ def body(mode):
             L.append("s_addc_u32 s43, s45, 0")
             L.append("s_swappc_b64 s[40:41], s[42:43]")
         L.append("s_set_gpr_idx_off")
+    elif mode == "call72r":  # idx mode, one table, coefficient varies per call (s49 = LCG state)
+        L.append("s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)")
+        for j in range(8):
+            if j:
+                L.append(f"s_set_gpr_idx_idx {8 * j}")
+            L += ["s_mul_i32 s49, s49, 0x41c64e6d", "s_add_u32 s49, s49, 12345",
+                  "s_lshr_b32 s50, s49, 24", "s_mul_i32 s50, s50, 72",
+                  "s_add_u32 s42, s44, s50", "s_addc_u32 s43, s45, 0", "s_swappc_b64 s[40:41], s[42:43]"]
+        L.append("s_set_gpr_idx_off")
+    elif mode == "call8r":  # no idx mode: 8 tables (one per accumulator set), random coefficients
+        for j in range(8):
+            L += ["s_mul_i32 s49, s49, 0x41c64e6d", "s_add_u32 s49, s49, 12345",
+                  "s_lshr_b32 s50, s49, 24", "s_mul_i32 s50, s50, 72",
+                  f"s_add_u32 s50, s50, {j * 257 * 72}",
+                  "s_add_u32 s42, s44, s50", "s_addc_u32 s43, s45, 0", "s_swappc_b64 s[40:41], s[42:43]"]
     elif mode == "direct":
         L.append("s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)")
         for j, c in enumerate(COEF):
@@ -101,17 +134,36 @@ def kernel(mode):
     if mode == "call128":
         pre = ["s_getpc_b64 s[44:45]", "s_add_u32 s44, s44, jp_tab128@rel32@lo+4", "s_addc_u32 s45, s45, jp_tab128@rel32@hi+12"]
         tables = ["s_branch jp_t128_end"] + table("jp_tab128", 7, ["s_setpc_b64 s[40:41]"]) + ["jp_t128_end:"]
+    if mode == "call72r":
+        pre = ["s_getpc_b64 s[44:45]", "s_add_u32 s44, s44, jp_tab72r@rel32@lo+4", "s_addc_u32 s45, s45, jp_tab72r@rel32@hi+12",
+               "s_mov_b32 s49, 1"]
+        tables = ["s_branch jp_t72r_end"] + table("jp_tab72r", 3, ["s_setpc_b64 s[40:41]"]) + ["jp_t72r_end:"]
+    if mode == "call8r":
+        pre = ["s_getpc_b64 s[44:45]", "s_add_u32 s44, s44, jp_tab8r@rel32@lo+4", "s_addc_u32 s45, s45, jp_tab8r@rel32@hi+12",
+               "s_mov_b32 s49, 1"]
+        t8 = ["s_getpc_b64 s[52:53]", "s_add_u32 s52, s52, jp_t8r_end@rel32@lo+4",
+              "s_addc_u32 s53, s53, jp_t8r_end@rel32@hi+12", "s_setpc_b64 s[52:53]", ".p2align 3", "jp_tab8r:"]
+        for j in range(8):
+            for c in range(257):
+                t8.append(".p2align 3")
+                v = c if c < 256 else 0
+                for bb in range(8):
+                    t8.append(f"v_bitop3_b32 v{ACC + 8 * j + bb}, v{ACC + 8 * j + bb}, v{T0 + (v & 15)}, v{T1 + (v >> 4)} bitop3:0x96")
+                    v = gmul2(v)
+                t8.append("s_setpc_b64 s[40:41]")
+        tables = t8 + ["jp_t8r_end:"]
     if mode == "setpc1":
         # one table per call site is too big; use a single return via a per-site SGPR pair:
         # snippet ends with s_setpc_b64 s[40:41], the caller loads s[40:41] with its return
         # address by s_getpc before the jump (no s_swappc), i.e. still two redirects -- measures
-        # the s_getpc+s_setpc form against s_swappc.
+        # the s_getpc+s_setpc form against s_swappc. s_getpc returns the address of the s_add that
+        # follows it; the return lands after the s_setpc: s_add (4 B, inline constant) + s_addc (4) + s_setpc (4).
         b = ["s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)"]
         for j, c in enumerate(COEF):
             if j:
                 b.append(f"s_set_gpr_idx_idx {8 * j}")
             b += [f"s_add_u32 s42, s46, {128 * c}", "s_addc_u32 s43, s47, 0", "s_getpc_b64 s[40:41]",
-                  "s_add_u32 s40, s40, 8", "s_addc_u32 s41, s41, 0", "s_setpc_b64 s[42:43]"]
+                  "s_add_u32 s40, s40, 12", "s_addc_u32 s41, s41, 0", "s_setpc_b64 s[42:43]"]
         b.append("s_set_gpr_idx_off")
         pre = ["s_getpc_b64 s[46:47]", "s_add_u32 s46, s46, jp_tabs1@rel32@lo+4", "s_addc_u32 s47, s47, jp_tabs1@rel32@hi+12"]
         tables = ["s_branch jp_ts1_end"] + table("jp_tabs1", 7, ["s_setpc_b64 s[40:41]"]) + ["jp_ts1_end:"]
@@ -127,7 +179,7 @@ def kernel(mode):
         "s_cmp_lt_u32 s48, %0\\n"
         "s_cbranch_scc1 jp_loop_{mode}\\n"
 {q(tables)}
-        :: "s"(iters) : {regs}, "s48", "scc", "memory");
+        :: "s"(iters) : {regs}, "s48", "s49", "s50", "s52", "s53", "scc", "memory");
     unsigned long long t1 = __builtin_amdgcn_s_memtime();
     unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
     if ((threadIdx.x & 63) == 0) {{
@@ -138,7 +190,7 @@ def kernel(mode):
 '''
 
 
-MODES = ["inline", "call72", "call128", "direct", "setpc1"]
+MODES = ["noidx", "inline", "call72", "call72r", "call8r"]
 
 
 def main():
@@ -176,6 +228,7 @@ int main(int argc, char **argv) {
             if (pass == 2)
                 printf("%-8s waves/SIMD=%d %.3f ms clock %.2f GHz  SIMD-cycles per product: %.1f (bitop3: %.2f)\n",
                        v.name, bpc, ms, ghz, ms * 1e-3 * ghz * 1e9 / products, ms * 1e-3 * ghz * 1e9 / products / 8);
+            fflush(stdout);
         }
     }
     return 0;
