@@ -78,3 +78,24 @@ def test_bench_two_ranks_on_one_gpu():
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["value"] > 0 and line["config"]["parallelism"] == "groups sharded x2"
     assert line["root_resident"].get("root_shard_roundtrip_ok") is True
+
+
+@pytest.mark.gpu
+def test_bench_total_groups_chunked_root_two_ranks():
+    """C5's form at small scale: `--total-groups` shards an odd number of groups unevenly over two
+    ranks ("scaling": "strong"), and the root-resident leg streams them through a small root
+    window in several chunks (partial last chunk on one rank) with the round trip checked."""
+    import json
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                        "--steps", "2", "--warmup", "1", "--total-groups", "301", "--root-chunk", "64",
+                        "--root-steps", "1", "--no-cpu", "--host-calls", "0", "--no-sweep"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert line["config"]["total_groups"] == 301
+    rr = line["root_resident"]
+    assert rr.get("root_shard_roundtrip_ok") is True, rr
+    assert rr["chunks"] == 3 and rr["chunk_groups_per_rank"] == 64

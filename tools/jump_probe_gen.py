@@ -88,6 +88,13 @@ def body(mode):
                   "s_lshr_b32 s50, s49, 24", "s_mul_i32 s50, s50, 72",
                   "s_add_u32 s42, s44, s50", "s_addc_u32 s43, s45, 0", "s_swappc_b64 s[40:41], s[42:43]"]
         L.append("s_set_gpr_idx_off")
+    elif mode in ("call4r", "call2r"):  # no idx mode: 4 / 2 tables, 8 products cycle over them
+        nt = 4 if mode == "call4r" else 2
+        for j in range(8):
+            L += ["s_mul_i32 s49, s49, 0x41c64e6d", "s_add_u32 s49, s49, 12345",
+                  "s_lshr_b32 s50, s49, 24", "s_mul_i32 s50, s50, 72",
+                  f"s_add_u32 s50, s50, {(j % nt) * 257 * 72}",
+                  "s_add_u32 s42, s44, s50", "s_addc_u32 s43, s45, 0", "s_swappc_b64 s[40:41], s[42:43]"]
     elif mode == "call8r":  # no idx mode: 8 tables (one per accumulator set), random coefficients
         for j in range(8):
             L += ["s_mul_i32 s49, s49, 0x41c64e6d", "s_add_u32 s49, s49, 12345",
@@ -138,12 +145,14 @@ def kernel(mode):
         pre = ["s_getpc_b64 s[44:45]", "s_add_u32 s44, s44, jp_tab72r@rel32@lo+4", "s_addc_u32 s45, s45, jp_tab72r@rel32@hi+12",
                "s_mov_b32 s49, 1"]
         tables = ["s_branch jp_t72r_end"] + table("jp_tab72r", 3, ["s_setpc_b64 s[40:41]"]) + ["jp_t72r_end:"]
-    if mode == "call8r":
-        pre = ["s_getpc_b64 s[44:45]", "s_add_u32 s44, s44, jp_tab8r@rel32@lo+4", "s_addc_u32 s45, s45, jp_tab8r@rel32@hi+12",
+    if mode in ("call8r", "call4r", "call2r"):
+        nt = {"call8r": 8, "call4r": 4, "call2r": 2}[mode]
+        lab = f"jp_tab{nt}r"
+        pre = ["s_getpc_b64 s[44:45]", f"s_add_u32 s44, s44, {lab}@rel32@lo+4", f"s_addc_u32 s45, s45, {lab}@rel32@hi+12",
                "s_mov_b32 s49, 1"]
-        t8 = ["s_getpc_b64 s[52:53]", "s_add_u32 s52, s52, jp_t8r_end@rel32@lo+4",
-              "s_addc_u32 s53, s53, jp_t8r_end@rel32@hi+12", "s_setpc_b64 s[52:53]", ".p2align 3", "jp_tab8r:"]
-        for j in range(8):
+        t8 = ["s_getpc_b64 s[52:53]", f"s_add_u32 s52, s52, {lab}_end@rel32@lo+4",
+              f"s_addc_u32 s53, s53, {lab}_end@rel32@hi+12", "s_setpc_b64 s[52:53]", ".p2align 3", f"{lab}:"]
+        for j in range(nt):
             for c in range(257):
                 t8.append(".p2align 3")
                 v = c if c < 256 else 0
@@ -151,7 +160,7 @@ def kernel(mode):
                     t8.append(f"v_bitop3_b32 v{ACC + 8 * j + bb}, v{ACC + 8 * j + bb}, v{T0 + (v & 15)}, v{T1 + (v >> 4)} bitop3:0x96")
                     v = gmul2(v)
                 t8.append("s_setpc_b64 s[40:41]")
-        tables = t8 + ["jp_t8r_end:"]
+        tables = t8 + [f"{lab}_end:"]
     if mode == "setpc1":
         # one table per call site is too big; use a single return via a per-site SGPR pair:
         # snippet ends with s_setpc_b64 s[40:41], the caller loads s[40:41] with its return
@@ -190,7 +199,7 @@ def kernel(mode):
 '''
 
 
-MODES = ["noidx", "inline", "call72", "call72r", "call8r"]
+MODES = ["noidx", "call72r", "call8r", "call4r", "call2r"]
 
 
 def main():
