@@ -275,7 +275,9 @@ const std::vector<TileLaunch> *tile_plan(Context &c, int k, int m, bool dec) {
         const int parts = (L.nrows + 7) / 8;
         const int S = sh::tile_steps_per_group(parts);
         L.tstride = static_cast<long long>((L.nsteps + S - 1) / S) * S * 8;
-        std::vector<uint32_t> t(static_cast<size_t>(parts) * L.tstride, addr(0));
+        // + 128 dwords of slack: a step slice's last scalar loads may run up to S - 1 steps past
+        // the part's table (into the next part's, or this slack after the last)
+        std::vector<uint32_t> t(static_cast<size_t>(parts) * L.tstride + 128, addr(0));
         for (int p = 0; p < parts; ++p)
             for (int x = 0; x < L.nsteps; ++x)
                 for (int j = 0; j < 8; ++j) {
@@ -314,13 +316,23 @@ hipError_t launch_fixed_batch(int k, int m, int B, int groups, const uint8_t *in
     return sh::launch_fixed(k, m, a, dec, s);
 }
 
+// Step slices of the single-group latency path: the k (+ m) serial ring steps of one group are
+// split over up to 8 workgroups, each XOR-ing its steps' products into a partial output, and the
+// partials are XOR-reduced (the products are linear). ~25 steps per slice.
+int latency_slices(int nsteps) { return std::max(1, std::min(8, nsteps / 25)); }
+
 // One pass of the tile kernels over the batch (encode, or decode stage A with position tables).
+// slice_scratch (groups == 1 only): room for latency_slices() partial outputs of m * B bytes;
+// the steps are then sliced and the partials XOR-reduced into `out`.
 int launch_tile_batch(Context &c, int k, int m, int B, int groups, const uint8_t *in, long long in_gs,
                       uint8_t *out, long long out_gs, const uint8_t *pos, const uint8_t *rpos, bool dec,
-                      hipStream_t s) {
+                      hipStream_t s, uint8_t *slice_scratch = nullptr) {
     const std::vector<TileLaunch> *plan = tile_plan(c, k, m, dec);
     if (!plan) return -2;
     for (const TileLaunch &L : *plan) {
+        const int parts = (L.nrows + 7) / 8;
+        const int S = sh::tile_steps_per_group(parts);
+        const int ns = (slice_scratch && groups == 1) ? latency_slices(L.nsteps) : 1;
         sh::TileArgs t{};
         t.f.in = in;
         t.f.in_gstride = in_gs;
@@ -340,14 +352,31 @@ int launch_tile_batch(Context &c, int k, int m, int B, int groups, const uint8_t
         t.row0 = L.row0;
         t.nrows = L.nrows;
         t.nsteps = L.nsteps;
-        SH_CHECK(sh::launch_tile(t, dec, s));
+        if (ns > 1) {
+            // slices of a multiple of S steps; partial p at slice_scratch + p * m * B (row r of the
+            // launch at + (row0 + r) * B, like the final output)
+            const int per = ((L.nsteps + ns - 1) / ns + S - 1) / S * S;
+            t.slice_steps = per;
+            t.slices = (L.nsteps + per - 1) / per;
+            t.out_slice_bytes = out_gs;
+            t.f.out = slice_scratch + static_cast<long long>(L.row0) * B;
+            t.f.out_bytes = out_gs - static_cast<long long>(L.row0) * B;
+            SH_CHECK(sh::launch_tile(t, dec, s));
+            SH_CHECK(sh::launch_xor_reduce(slice_scratch + static_cast<long long>(L.row0) * B, out_gs, t.slices,
+                                           out + static_cast<long long>(L.row0) * B,
+                                           static_cast<long long>(L.nrows) * B, s));
+        } else {
+            SH_CHECK(sh::launch_tile(t, dec, s));
+        }
     }
     return 0;
 }
 
 // ---- batched encode ----
+// slice_scratch (single-group ABI): 8 * m * B device bytes that let one group's steps run as
+// parallel slices on the tile kernels (latency); nullptr = the throughput kernels.
 int encode_batch(int k, int m, int B, int groups, const uint8_t *d_in, uint8_t *d_out,
-                 hipStream_t s) {
+                 hipStream_t s, uint8_t *slice_scratch = nullptr) {
     Context &c = ctx();
     DeviceScope ds(c);
     if (ds.rc) return ds.rc;
@@ -364,13 +393,15 @@ int encode_batch(int k, int m, int B, int groups, const uint8_t *d_in, uint8_t *
         SH_CHECK(sh::launch_xor_rows(d_in, in_gs, k, d_out, out_gs, B, groups, s));
         return (m == 1 || valid) ? 0 : -1;  // m == 1 returns before validation (:1503-1506)
     }
-    if (sh::has_fixed(k, m, B) && !force_tile()) {
+    const bool sliced = slice_scratch && groups == 1 && tile_usable(c, k, m, B) && latency_slices(k) > 1;
+    if (sh::has_fixed(k, m, B) && !force_tile() && !sliced) {
         SH_CHECK(launch_fixed_batch(k, m, B, groups, d_in, in_gs, d_out, out_gs, nullptr, nullptr,
                                     false, s));
         return 0;
     }
     if (tile_usable(c, k, m, B))
-        return launch_tile_batch(c, k, m, B, groups, d_in, in_gs, d_out, out_gs, nullptr, nullptr, false, s);
+        return launch_tile_batch(c, k, m, B, groups, d_in, in_gs, d_out, out_gs, nullptr, nullptr, false, s,
+                                 sliced ? slice_scratch : nullptr);
     uint8_t *gen = generator(c, k, m);
     if (!gen) return -2;
     sh::ApplyArgs a{};
@@ -520,7 +551,8 @@ hipError_t launch_stage_b(const DecodeWS &w, int n_in, int B, int groups, uint8_
 // Common decode core (m >= 2, valid params): writes recovered blocks densely into `dst`
 // ([G][emax][B]) and leaves per-group e / rec_idx / erasures in the workspace.
 int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_blocks,
-                const uint8_t *d_rows, DecodeWS &w, int *errors, uint8_t *dst, hipStream_t s) {
+                const uint8_t *d_rows, DecodeWS &w, int *errors, uint8_t *dst, hipStream_t s,
+                uint8_t *slice_scratch = nullptr) {
     uint8_t *gen = generator(c, k, m);
     if (!gen) return -2;
     sh::DecodeSetupArgs sa{};
@@ -567,11 +599,13 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
     if (w.fixed) {
         // Stage A (compile-time generator, all m rows, erased columns read as zeros):
         //   residual_y = R_y + sum_{received x} M(C[y][x]) d_x
-        if (sh::has_fixed(k, m, B) && !force_tile()) {
+        const bool sliced = slice_scratch && groups == 1 && tile_usable(c, k, m, B) && latency_slices(k + m) > 1;
+        if (sh::has_fixed(k, m, B) && !force_tile() && !sliced) {
             SH_CHECK(launch_fixed_batch(k, m, B, groups, d_blocks, static_cast<long long>(k) * B,
                                         w.residual, static_cast<long long>(m) * B, w.pos, w.rpos, true, s));
         } else if (int rc = launch_tile_batch(c, k, m, B, groups, d_blocks, static_cast<long long>(k) * B,
-                                              w.residual, static_cast<long long>(m) * B, w.pos, w.rpos, true, s)) {
+                                              w.residual, static_cast<long long>(m) * B, w.pos, w.rpos, true, s,
+                                              sliced ? slice_scratch : nullptr)) {
             return rc;
         }
         if (ev) SH_CHECK(hipEventRecord(ev[2], s));
@@ -615,7 +649,7 @@ int invalid_decode_status(int k, int groups, const uint8_t *d_rows, hipStream_t 
 // e_host (optional, pinned host memory): receives group 0's e, copied on `s` while the workspace
 // is still leased to this call (the single-group ABI reads it after synchronising).
 int decode_batch(int k, int m, int B, int groups, uint8_t *d_blocks, uint8_t *d_rows,
-                 hipStream_t s, int *e_host = nullptr) {
+                 hipStream_t s, int *e_host = nullptr, uint8_t *slice_scratch = nullptr) {
     Context &c = ctx();
     DeviceScope ds(c);
     if (ds.rc) return ds.rc;
@@ -633,7 +667,8 @@ int decode_batch(int k, int m, int B, int groups, uint8_t *d_blocks, uint8_t *d_
     WsLease ls;
     if (int rc = lease_workspace(c, s, carve(w, nullptr, k, m, B, groups, true), ls)) return rc;
     carve(w, ls.p, k, m, B, groups, true);
-    if (int rc = decode_core(c, k, m, B, groups, d_blocks, d_rows, w, ls.errors, w.recovered, s)) return rc;
+    if (int rc = decode_core(c, k, m, B, groups, d_blocks, d_rows, w, ls.errors, w.recovered, s, slice_scratch))
+        return rc;
     sh::ScatterArgs sc{};
     sc.src = w.recovered;
     sc.src_gstride = static_cast<long long>(w.emax) * B;
@@ -867,13 +902,14 @@ extern "C" int cauchy_256_encode(int k, int m, const unsigned char *data_ptrs[],
     const size_t in_bytes = static_cast<size_t>(kin) * block_bytes;
     const size_t out_bytes = static_cast<size_t>(m) * block_bytes;
     std::lock_guard<std::mutex> g(c.stage_mu);  // one staging area; calls serialise like Shorthair's
+    const size_t scratch = 8 * out_bytes;      // step-slice partials (latency path)
     if (int rc = c.h_stage.ensure(in_bytes + out_bytes)) return rc;
-    if (int rc = c.d_stage.ensure(in_bytes + out_bytes)) return rc;
+    if (int rc = c.d_stage.ensure(in_bytes + out_bytes + scratch)) return rc;
     uint8_t *h = static_cast<uint8_t *>(c.h_stage.p);
     uint8_t *d = static_cast<uint8_t *>(c.d_stage.p);
     for (int x = 0; x < kin; ++x) std::memcpy(h + static_cast<size_t>(x) * block_bytes, data_ptrs[x], block_bytes);
     SH_CHECK(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, c.stream));
-    const int rc = encode_batch(k, m, block_bytes, 1, d, d + in_bytes, c.stream);
+    const int rc = encode_batch(k, m, block_bytes, 1, d, d + in_bytes, c.stream, d + in_bytes + out_bytes);
     if (rc == -2) return rc;
     // Like the reference, a rejected call has still written recovery row 0.
     const size_t copy = (rc == 0) ? out_bytes : static_cast<size_t>(block_bytes);
@@ -894,8 +930,9 @@ extern "C" int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes) {
     if (block_bytes <= 0) return 0;
     const size_t data_bytes = static_cast<size_t>(k) * block_bytes;
     std::lock_guard<std::mutex> g(c.stage_mu);
+    const size_t scratch = 8 * static_cast<size_t>(std::max(m, 1)) * block_bytes;  // step-slice partials
     if (int rc = c.h_stage.ensure(data_bytes + 256 + 8)) return rc;
-    if (int rc = c.d_stage.ensure(data_bytes + 256)) return rc;
+    if (int rc = c.d_stage.ensure(data_bytes + 256 + scratch)) return rc;
     uint8_t *h = static_cast<uint8_t *>(c.h_stage.p);
     uint8_t *d = static_cast<uint8_t *>(c.d_stage.p);
     for (int i = 0; i < k; ++i) {
@@ -906,7 +943,7 @@ extern "C" int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes) {
     int *e_host = reinterpret_cast<int *>(h + ((data_bytes + k + 3) & ~static_cast<size_t>(3)));
     *e_host = 0;
     SH_CHECK(hipMemcpyAsync(d, h, data_bytes + k, hipMemcpyHostToDevice, c.stream));
-    const int rc = decode_batch(k, m, block_bytes, 1, d, d + data_bytes, c.stream, e_host);
+    const int rc = decode_batch(k, m, block_bytes, 1, d, d + data_bytes, c.stream, e_host, d + data_bytes + 256);
     if (rc != 0) return rc;
     SH_CHECK(hipMemcpyAsync(h, d, data_bytes + k, hipMemcpyDeviceToHost, c.stream));
     SH_CHECK(hipStreamSynchronize(c.stream));

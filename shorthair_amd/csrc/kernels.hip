@@ -536,6 +536,33 @@ __global__ void decode_k1(uint8_t *rows, long long rows_gstride, int groups) {
     if (g < groups) rows[g * rows_gstride] = 0;
 }
 
+// XOR of the step slices' partial outputs (single-group latency path): one thread per dword.
+__global__ __launch_bounds__(256) void xor_reduce(const uint8_t *parts, long long part_bytes, int nparts,
+                                                  uint8_t *out, long long nbytes) {
+    const long long i = (static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x) * 4;
+    if (i >= nbytes) return;
+    if (i + 4 <= nbytes && (part_bytes & 3) == 0) {
+        uint32_t x = ld32(parts + i);
+        for (int p = 1; p < nparts; ++p) x ^= ld32(parts + p * part_bytes + i);
+        st32(out + i, x);
+    } else {
+        for (long long b = i; b < nbytes && b < i + 4; ++b) {
+            uint8_t x = parts[b];
+            for (int p = 1; p < nparts; ++p) x ^= parts[p * part_bytes + b];
+            out[b] = x;
+        }
+    }
+}
+
+hipError_t launch_xor_reduce(const uint8_t *parts, long long part_bytes, int nparts, uint8_t *out,
+                             long long nbytes, hipStream_t stream) {
+    if (nbytes <= 0) return hipSuccess;
+    const long long threads = (nbytes + 3) / 4;
+    hipLaunchKernelGGL(xor_reduce, dim3(static_cast<unsigned>((threads + 255) / 256)), dim3(256), 0, stream,
+                       parts, part_bytes, nparts, out, nbytes);
+    return hipGetLastError();
+}
+
 // Synthetic workload (same stream as oracle/cauchy_oracle.c ora_fill_block): block x of group g
 // is PCG32 Seed(g*256 + x, cfg) output words, little-endian. One thread per block.
 __device__ __forceinline__ uint32_t pcg_next(uint64_t &state, uint64_t inc) {

@@ -162,6 +162,11 @@ struct TileArgs {
     long long tstride;
     uint32_t snip_hi;         // high dword of every snippet address
     int k, m, row0, nrows, nsteps;
+    // Step slices (single-group latency): slice s = blockIdx.y codes steps [s*slice_steps, ...)
+    // into its own partial output at f.out + s * out_slice_bytes (XOR-reduced afterwards).
+    // slice_steps = 0: one slice over every step.
+    int slice_steps, slices;
+    long long out_slice_bytes;
 };
 bool tile_ok(int B);
 int tile_steps_per_group(int parts);
@@ -182,6 +187,9 @@ hipError_t launch_scatter(const ScatterArgs &a, int groups, hipStream_t stream);
 hipError_t launch_decode_m1(uint8_t *blocks, long long blocks_gstride, const uint8_t *rows,
                             long long rows_gstride, int k, int B, int groups, hipStream_t stream);
 hipError_t launch_decode_k1(uint8_t *rows, long long rows_gstride, int groups, hipStream_t stream);
+// out[i] = XOR over p < nparts of parts[p * part_bytes + i], i < nbytes (the slices' partials).
+hipError_t launch_xor_reduce(const uint8_t *parts, long long part_bytes, int nparts, uint8_t *out,
+                             long long nbytes, hipStream_t stream);
 hipError_t launch_fill(uint8_t *out, long long gstride, int n, int B, int groups,
                        unsigned long long g0, unsigned long long cfg, hipStream_t stream);
 

@@ -60,7 +60,7 @@ struct TSrc {
     uint32_t dbase[S::DPW];
     int dgl[S::DPW];
     uint32_t B;
-    int wave, n, k, kp, pstride, row0;
+    int wave, n, x0, k, kp, pstride, row0;
     uint32_t rd;
     uint8_t *lds;
     const uint8_t *pos;
@@ -74,7 +74,8 @@ struct TSrc {
         lds = lds_ring;
         pos = lds_pos;
         wave = w.wave;
-        n = t.nsteps;
+        x0 = t.slice_steps > 0 ? static_cast<int>(blockIdx.y) * t.slice_steps : 0;
+        n = t.slice_steps > 0 ? min(t.slice_steps, t.nsteps - x0) : t.nsteps;
         k = t.k;
         kp = (t.k + 3) & ~3;
         pstride = kp + ((t.m + 3) & ~3);
@@ -106,13 +107,14 @@ struct TSrc {
             lds_void *dst = (lds_void *)(slot + (wave * S::DPW + j) * 64 * S::W);
             uint32_t o = OOR, so = 0;
             if (x < n && dbase[j] != OOR) {
+                const int gx = x0 + x;  // step of the whole range
                 if (DEC) {
-                    const int t = x < k ? x : kp + row0 + (x - k);
+                    const int t = gx < k ? gx : kp + row0 + (gx - k);
                     const int p = pos[dgl[j] * pstride + t];
                     o = p == 0xFF ? OOR : dbase[j] + static_cast<uint32_t>(p) * B;
                 } else {
                     o = dbase[j];
-                    so = static_cast<uint32_t>(x) * B;
+                    so = static_cast<uint32_t>(gx) * B;
                 }
             }
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, S::W, o, so, 0, 0);
@@ -269,11 +271,16 @@ __device__ __forceinline__ void tile_body(const TileArgs &t) {
     TSrc<S, DEC> src;
     src.init(t, w, lds, lds_pos);
     RowSink<S> sink;
-    sink.init(a, w, part, lds);
+    FixedArgs so = a;  // this slice's partial output
+    if (t.slice_steps > 0) {
+        so.out += static_cast<long long>(blockIdx.y) * t.out_slice_bytes;
+        so.out_bytes = t.out_slice_bytes;
+    }
+    sink.init(so, w, part, lds);
 
     // snippet-address low dwords of this part: [ngroups * S steps][8], scalar loads
     typedef const __attribute__((address_space(4))) uint32_t cu32_t;
-    const cu32_t *tp = (const cu32_t *)(t.targets + static_cast<long long>(part) * t.tstride);
+    const cu32_t *tp = (const cu32_t *)(t.targets + static_cast<long long>(part) * t.tstride + 8ll * src.x0);
     const uint32_t hi = t.snip_hi;
 
     Acc A;
@@ -281,7 +288,7 @@ __device__ __forceinline__ void tile_body(const TileArgs &t) {
     for (int i = 0; i < 16; ++i) A.a01[i] = A.a23[i] = A.a45[i] = A.a67[i] = 0;
     A.z0 = A.z1 = 0;
 
-    const int n = t.nsteps;
+    const int n = src.n;
     const int ngroups = (n + S::S - 1) / S::S;
     for (int x = 0; x < S::R - 1; ++x) src.issue(x);
     src.template wait<S::R - S::S - 1>();
@@ -352,7 +359,8 @@ hipError_t launch_p(const TileArgs &t0, bool dec, hipStream_t s, void (*ke)(Tile
     const size_t lds = static_cast<size_t>(S::R) * S::SLOT + (dec ? static_cast<size_t>(t.f.groups_per_wg) * (kp + mp) : 0);
     const long long cols = static_cast<long long>(t.f.groups) * t.f.geo.nq;
     const unsigned blocks = static_cast<unsigned>((cols + S::COLS - 1) / S::COLS);
-    hipLaunchKernelGGL(dec ? kd : ke, dim3(blocks), dim3(S::NT), lds, s, t);
+    const unsigned slices = t.slice_steps > 0 ? static_cast<unsigned>(t.slices) : 1u;
+    hipLaunchKernelGGL(dec ? kd : ke, dim3(blocks, slices), dim3(S::NT), lds, s, t);
     return hipGetLastError();
 }
 
