@@ -436,14 +436,16 @@ struct DecodeWS {
     long long coefA_gs, coefB_gs;
 };
 
-// Stage B after a full-residual stage A: stageb_v2 for 16 < emax <= 64, where it measured faster
-// ((200,32) e = 32: 0.34 vs 0.39 ms; (200,56) e = 56: 0.667 vs 0.741 ms); round 2's kernels with
-// setup-written snippet addresses elsewhere: stageb_regs for emax <= 16 (C2 decode 0.72 vs 0.79 ms,
-// (28,4,1400) 0.51 vs 0.66 ms) and stageb_fixed above 64 ((190,66) decode 2.57 vs 2.89 ms).
-// SH_STAGEB_OLD=1 (measurement switch) selects round 2's kernels everywhere.
+// Stage B after a full-residual stage A: stageb_v2 for emax > 16, where it measured faster
+// ((200,32) e = 32: 0.34 vs 0.39 ms; (200,56) e = 56: 0.478 vs 0.532 ms; (190,66) e = 66: 0.763 vs
+// 0.838 ms and (120,136) e = 120: 1.77 vs 2.07 ms against stageb_fixed, with 4- or 8-wave chunks,
+// stageb.hip); round 2's stageb_regs with setup-written snippet addresses for emax <= 16 (C2 decode
+// 0.72 vs 0.79 ms, (28,4,1400) 0.51 vs 0.66 ms). SH_STAGEB_OLD=1 (measurement switch) selects
+// round 2's kernels everywhere; SH_V2_MAX caps the emax served by stageb_v2.
 bool stageb_v2_on(const sh::Geometry &geo, int emax) {
     static const bool old = std::getenv("SH_STAGEB_OLD") != nullptr;
-    return !old && emax > 16 && emax <= 64 && sh::stageb_v2_ok(geo, emax);
+    static const int vmax = std::getenv("SH_V2_MAX") ? std::atoi(std::getenv("SH_V2_MAX")) : 128;  // measurement
+    return !old && emax > 16 && emax <= vmax && sh::stageb_v2_ok(geo, emax);
 }
 
 size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool need_recovered) {

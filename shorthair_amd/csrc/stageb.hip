@@ -22,6 +22,7 @@
 #include "snippets.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace sh {
 
@@ -641,18 +642,21 @@ hipError_t launch_stageb_v2(const StageBV2Args &a, hipStream_t stream) {
     if (!stageb_v2_ok(a.geo, a.emax)) return hipErrorNotSupported;
     const int ncc = (a.geo.nq + 63) / 64;
     const int octets = (a.emax + 7) / 8;
-    // Output chunks of <= 8 waves (64 outputs) per workgroup, as few as possible (each chunk
-    // streams all e rows), split evenly: 4..8 waves (4 waves per SIMD at 128 VGPRs).
-    const int chunks = (octets + 7) / 8;
-    const int nw = std::max(4, (octets + chunks - 1) / chunks);
-    dim3 grid(static_cast<unsigned>(ncc) * a.groups, (octets + nw - 1) / nw, 1);
-    switch (nw) {
-        case 4: hipLaunchKernelGGL(stageb_v2<4>, grid, dim3(256), 0, stream, a); break;
-        case 5: hipLaunchKernelGGL(stageb_v2<5>, grid, dim3(320), 0, stream, a); break;
-        case 6: hipLaunchKernelGGL(stageb_v2<6>, grid, dim3(384), 0, stream, a); break;
-        case 7: hipLaunchKernelGGL(stageb_v2<7>, grid, dim3(448), 0, stream, a); break;
-        default: hipLaunchKernelGGL(stageb_v2<8>, grid, dim3(512), 0, stream, a); break;
-    }
+    // Output chunks of 4 or 8 waves (32 or 64 outputs) per workgroup: a wave count that is not a
+    // multiple of the CU's 4 SIMDs leaves one SIMD with an extra wave of every workgroup (5-7 waves
+    // measured 10 % slower at e = 56, 66). Each chunk streams all e rows, so 8-wave chunks unless
+    // 4-wave chunks need fewer wave slots (e = 66: 3 x 4 waves, 9 active, vs 2 x 8 with 7 idle):
+    // (200,56,1352) stage B 0.478 vs 0.532 ms (7 waves), (190,66,1336) 0.763 vs 0.838 ms
+    // (stageb_fixed), (120,136,1400) 1.772 vs 2.070 ms (4096 groups).
+    static const int force = std::getenv("SH_V2_NW") ? std::atoi(std::getenv("SH_V2_NW")) : 0;  // measurement
+    const int c4 = (octets + 3) / 4, c8 = (octets + 7) / 8;
+    const int nw = force ? force : (8 * c8 <= 4 * c4 ? 8 : 4);
+    const int chunks = (octets + nw - 1) / nw;
+    dim3 grid(static_cast<unsigned>(ncc) * a.groups, chunks, 1);
+    if (nw == 4)
+        hipLaunchKernelGGL(stageb_v2<4>, grid, dim3(256), 0, stream, a);
+    else
+        hipLaunchKernelGGL(stageb_v2<8>, grid, dim3(512), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -240,7 +240,8 @@ def shape(k, m):
     nw = CW * P
     slot = 8 * CW * 64 * 4
     rmax = int(os.environ.get("SH_RING_MAX", "19"))
-    R = int(os.environ.get("SH_RING", str(max(3, min(rmax, 65536 // slot, (76 * 1024) // slot)))))
+    rbytes = int(os.environ.get("SH_RING_BYTES", "65536"))  # > 64 KB: with -DSH_RING_LIMIT (experiments)
+    R = int(os.environ.get("SH_RING", str(max(3, min(rmax, rbytes // slot, (76 * 1024) // slot)))))
     rows = (m + P - 1) // P
     minw = int(os.environ.get("SH_MIN_WAVES", "2" if rows > 12 else ("3" if rows > 8 else "4")))
     # blocks per barrier: R >= 2*SYNC + 1 keeps >= 1 group of DMA in flight past the one waited for

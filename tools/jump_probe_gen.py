@@ -60,6 +60,7 @@ def body(mode):
         for j, c in enumerate(COEF):
             if j:
                 L.append(f"s_set_gpr_idx_idx {8 * j}")
+                L.append("s_nop 1")
             L += snippet(c, [])
         L.append("s_set_gpr_idx_off")
     elif mode == "inline":
@@ -78,6 +79,41 @@ def body(mode):
             L.append(f"s_add_u32 s42, s44, {stride * c}")
             L.append("s_addc_u32 s43, s45, 0")
             L.append("s_swappc_b64 s[40:41], s[42:43]")
+        L.append("s_set_gpr_idx_off")
+    elif mode == "v2":  # stage B v2's form: snippet address from a coefficient word by SALU
+        L.append("s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)")
+        for j in range(8):
+            if j:
+                L.append(f"s_set_gpr_idx_idx {8 * j}")
+            w = "s50" if j < 4 else "s51"
+            L += [f"s_bfe_u32 s42, {w}, {0x80000 + 8 * (j % 4)}", "s_lshl3_add_u32 s42, s42, s42",
+                  "s_lshl3_add_u32 s42, s42, s44", "s_mov_b32 s43, s45", "s_swappc_b64 s[40:41], s[42:43]"]
+        L.append("s_set_gpr_idx_off")
+    elif mode == "rl":  # snippet address low dwords from a VGPR (lane j) by v_readlane, before idx mode
+        # (in VGPR-index mode SRC0 of v_readlane would be M0-relative)
+        L += [f"v_readlane_b32 s{52 + j}, v20, {j}" for j in range(8)]
+        L.append("s_mov_b32 s43, s45")
+        L.append("s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)")
+        for j in range(8):
+            if j:
+                L.append(f"s_set_gpr_idx_idx {8 * j}")
+            L += [f"s_mov_b32 s42, s{52 + j}", "s_swappc_b64 s[40:41], s[42:43]"]
+        L.append("s_set_gpr_idx_off")
+    elif mode in ("call1", "callidx0"):  # 8 calls per iteration, no M0 change (call1: no idx mode at all)
+        if mode == "callidx0":
+            L.append("s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)")
+        L += ["s_mov_b32 s43, s45"]
+        for j in range(8):
+            L += [f"s_bfe_u32 s42, {'s50' if j < 4 else 's51'}, {0x80000 + 8 * (j % 4)}", "s_lshl3_add_u32 s42, s42, s42",
+                  "s_lshl3_add_u32 s42, s42, s44", "s_swappc_b64 s[40:41], s[42:43]"]
+        if mode == "callidx0":
+            L.append("s_set_gpr_idx_off")
+    elif mode == "m0mov":  # as inline, M0 set by s_mov_b32 m0 instead of s_set_gpr_idx_idx
+        L.append("s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)")
+        for j, c in enumerate(COEF):
+            if j:
+                L.append(f"s_mov_b32 m0, {8 * j}")
+            L += snippet(c, [])
         L.append("s_set_gpr_idx_off")
     elif mode == "call72r":  # idx mode, one table, coefficient varies per call (s49 = LCG state)
         L.append("s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)")
@@ -141,6 +177,14 @@ def kernel(mode):
     if mode == "call128":
         pre = ["s_getpc_b64 s[44:45]", "s_add_u32 s44, s44, jp_tab128@rel32@lo+4", "s_addc_u32 s45, s45, jp_tab128@rel32@hi+12"]
         tables = ["s_branch jp_t128_end"] + table("jp_tab128", 7, ["s_setpc_b64 s[40:41]"]) + ["jp_t128_end:"]
+    if mode in ("v2", "rl", "call1", "callidx0"):
+        pre = ["s_getpc_b64 s[44:45]", "s_add_u32 s44, s44, jp_tab72" + mode + "@rel32@lo+4", "s_addc_u32 s45, s45, jp_tab72" + mode + "@rel32@hi+12",
+               "s_mov_b32 s50, 0x8e1fca53", "s_mov_b32 s51, 0xd967b235"]
+        if mode == "rl":
+            pre += ["v_mbcnt_lo_u32_b32 v21, -1, 0", "v_mbcnt_hi_u32_b32 v21, -1, v21", "v_and_b32 v21, 7, v21",
+                    "v_mul_u32_u24 v21, 41, v21", "v_and_b32 v21, 255, v21", "v_mul_u32_u24 v21, 72, v21",
+                    "v_add_u32 v20, s44, v21"]
+        tables = ["s_branch jp_t72e" + mode] + table("jp_tab72" + mode, 3, ["s_setpc_b64 s[40:41]", "s_nop 0"]) + ["jp_t72e" + mode + ":"]
     if mode == "call72r":
         pre = ["s_getpc_b64 s[44:45]", "s_add_u32 s44, s44, jp_tab72r@rel32@lo+4", "s_addc_u32 s45, s45, jp_tab72r@rel32@hi+12",
                "s_mov_b32 s49, 1"]
@@ -188,7 +232,7 @@ def kernel(mode):
         "s_cmp_lt_u32 s48, %0\\n"
         "s_cbranch_scc1 jp_loop_{mode}\\n"
 {q(tables)}
-        :: "s"(iters) : {regs}, "s48", "s49", "s50", "s52", "s53", "scc", "memory");
+        :: "s"(iters) : {regs}, "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "v20", "v21", "scc", "memory");
     unsigned long long t1 = __builtin_amdgcn_s_memtime();
     unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
     if ((threadIdx.x & 63) == 0) {{
@@ -199,7 +243,7 @@ def kernel(mode):
 '''
 
 
-MODES = ["noidx", "call72r", "call8r", "call4r", "call2r"]
+MODES = ["noidx", "idx0", "inline", "idxnop", "m0mov", "call1", "callidx0", "v2"]
 
 
 def main():
