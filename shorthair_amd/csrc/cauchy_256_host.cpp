@@ -272,7 +272,7 @@ const std::vector<TileLaunch> *tile_plan(Context &c, int k, int m, bool dec) {
         L.row0 = row0;
         L.nrows = std::min(128, m - row0);
         L.nsteps = k + (dec ? L.nrows : 0);
-        const int parts = (L.nrows + 7) / 8;
+        const int parts = sh::tile_parts(L.nrows);
         const int S = sh::tile_steps_per_group(parts);
         L.tstride = static_cast<long long>((L.nsteps + S - 1) / S) * S * 8;
         // + 128 dwords of slack: a step slice's last scalar loads may run up to S - 1 steps past
@@ -281,8 +281,9 @@ const std::vector<TileLaunch> *tile_plan(Context &c, int k, int m, bool dec) {
         for (int p = 0; p < parts; ++p)
             for (int x = 0; x < L.nsteps; ++x)
                 for (int j = 0; j < 8; ++j) {
-                    const int yy = 8 * p + j;
-                    if (yy >= L.nrows) continue;
+                    // part p: rows [p * nrows / parts, (p + 1) * nrows / parts) (tile_snip.hip)
+                    const int yy = p * L.nrows / parts + j;
+                    if (yy >= (p + 1) * L.nrows / parts) continue;
                     const int cf = x < k ? G[static_cast<size_t>(row0 + yy) * k + x] : (x - k == yy ? 1 : 0);
                     t[static_cast<size_t>(p) * L.tstride + static_cast<size_t>(x) * 8 + j] = addr(cf);
                 }
@@ -330,7 +331,7 @@ int launch_tile_batch(Context &c, int k, int m, int B, int groups, const uint8_t
     const std::vector<TileLaunch> *plan = tile_plan(c, k, m, dec);
     if (!plan) return -2;
     for (const TileLaunch &L : *plan) {
-        const int parts = (L.nrows + 7) / 8;
+        const int parts = sh::tile_parts(L.nrows);
         const int S = sh::tile_steps_per_group(parts);
         const int ns = (slice_scratch && groups == 1) ? latency_slices(L.nsteps) : 1;
         sh::TileArgs t{};

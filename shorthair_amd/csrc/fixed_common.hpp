@@ -103,10 +103,9 @@ struct Shape {
     static constexpr int NDMA = SLOT / (64 * W);        // DMA wave-instructions per step
     static constexpr int DPW = (NDMA + NW - 1) / NW;    // ... issued by each wave (at most)
     static constexpr int KP = (K + 3) & ~3, MP = (M + 3) & ~3;
-#ifndef SH_RING_LIMIT
-#define SH_RING_LIMIT 65536  // ds_read's 16-bit offsets reach every slot (larger: experiments only)
-#endif
-    static_assert(R >= 3 && R * SLOT <= SH_RING_LIMIT, "ring must fit ds_read's 16-bit offsets");
+    // <= 64 KB: two workgroups per CU, and ds_read's 16-bit offsets reach every slot; the 16-wave
+    // shapes (one workgroup per CU) take 128 KB (slot offsets past 64 KB cost an address add)
+    static_assert(R >= 3 && R * SLOT <= (NW >= 16 ? 131072 : 65536), "ring size");
 };
 
 // Per-lane geometry shared by the source and the sink.

@@ -169,6 +169,7 @@ struct TileArgs {
     long long out_slice_bytes;
 };
 bool tile_ok(int B);
+int tile_parts(int nrows);
 int tile_steps_per_group(int parts);
 hipError_t launch_tile(const TileArgs &t, bool dec, hipStream_t stream);
 

@@ -138,8 +138,9 @@ struct TSrc {
 };
 
 // One step of a part-wave: window tables of the step's 8 words into v[96:127] (v96 = v112 = 0
-// are the zero entries), then 8 snippet calls, call j in VGPR-index mode with M0 = 8j so the
-// snippet's destination and first source are accumulator set j (v[32+8j .. 32+8j+7]).
+// are the zero entries), then one snippet call per row of the part (nr, 4..8: calls 4..7 are
+// skipped past the part's last row), call j in VGPR-index mode with M0 = 8j so the snippet's
+// destination and first source are accumulator set j (v[32+8j .. 32+8j+7]).
 #define SH_TILE_STEP_ASM                                                                          \
     "v_mov_b32 v97, %[d0]\n"                                                                      \
     "v_mov_b32 v98, %[d1]\n"                                                                      \
@@ -184,18 +185,27 @@ struct TSrc {
     "s_set_gpr_idx_idx 24\n"                                                                      \
     "s_mov_b32 s42, %[g3]\n"                                                                      \
     "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
+    "s_cmp_le_u32 %[nr], 4\n"                                                                     \
+    "s_cbranch_scc1 9f\n"                                                         \
     "s_set_gpr_idx_idx 32\n"                                                                      \
     "s_mov_b32 s42, %[g4]\n"                                                                      \
     "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
+    "s_cmp_le_u32 %[nr], 5\n"                                                                     \
+    "s_cbranch_scc1 9f\n"                                                         \
     "s_set_gpr_idx_idx 40\n"                                                                      \
     "s_mov_b32 s42, %[g5]\n"                                                                      \
     "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
+    "s_cmp_le_u32 %[nr], 6\n"                                                                     \
+    "s_cbranch_scc1 9f\n"                                                         \
     "s_set_gpr_idx_idx 48\n"                                                                      \
     "s_mov_b32 s42, %[g6]\n"                                                                      \
     "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
+    "s_cmp_le_u32 %[nr], 7\n"                                                                     \
+    "s_cbranch_scc1 9f\n"                                                         \
     "s_set_gpr_idx_idx 56\n"                                                                      \
     "s_mov_b32 s42, %[g7]\n"                                                                      \
     "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
+    "9:\n"                                                                       \
     "s_set_gpr_idx_off"
 
 struct Acc {
@@ -203,18 +213,18 @@ struct Acc {
     uint32_t z0, z1;
 };
 
-__device__ __forceinline__ void step(const uint32_t (&d)[8], const uint32_t *g, uint32_t hi, Acc &A) {
+__device__ __forceinline__ void step(const uint32_t (&d)[8], const uint32_t *g, uint32_t hi, uint32_t nr, Acc &A) {
     asm volatile(SH_TILE_STEP_ASM
                  : "+{v[32:47]}"(A.a01), "+{v[48:63]}"(A.a23), "+{v[64:79]}"(A.a45), "+{v[80:95]}"(A.a67),
                    "+{v96}"(A.z0), "+{v112}"(A.z1)
                  : [d0] "v"(d[0]), [d1] "v"(d[1]), [d2] "v"(d[2]), [d3] "v"(d[3]), [d4] "v"(d[4]),
                    [d5] "v"(d[5]), [d6] "v"(d[6]), [d7] "v"(d[7]), [g0] "s"(g[0]), [g1] "s"(g[1]),
                    [g2] "s"(g[2]), [g3] "s"(g[3]), [g4] "s"(g[4]), [g5] "s"(g[5]), [g6] "s"(g[6]),
-                   [g7] "s"(g[7]), [hi] "s"(hi)
+                   [g7] "s"(g[7]), [hi] "s"(hi), [nr] "s"(nr)
                  : "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107",
                    "v108", "v109", "v110", "v111", "v113", "v114", "v115", "v116", "v117", "v118", "v119",
                    "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "s40", "s41", "s42",
-                   "s43", "m0", "memory");
+                   "s43", "m0", "scc", "memory");
 }
 
 // Every wave joins one barrier per row of a part (8), storing its part's rows < nr.
@@ -282,6 +292,9 @@ __device__ __forceinline__ void tile_body(const TileArgs &t) {
     typedef const __attribute__((address_space(4))) uint32_t cu32_t;
     const cu32_t *tp = (const cu32_t *)(t.targets + static_cast<long long>(part) * t.tstride + 8ll * src.x0);
     const uint32_t hi = t.snip_hi;
+    // this part's rows [y0, y0 + nr): the launch's rows split evenly over the P parts (4..8 each)
+    const int y0 = part * t.nrows / S::P;
+    const int nr = (part + 1) * t.nrows / S::P - y0;
 
     Acc A;
 #pragma unroll
@@ -309,7 +322,7 @@ __device__ __forceinline__ void tile_body(const TileArgs &t) {
                 for (int u = 0; u < S::S; ++u) src.issue(i + S::R - S::S + u);
             }
             if (i + 1 < n) src.read((i + 1) % S::R, nxt);
-            if (i < n) step(cur, &gl[r * 8], hi, A);
+            if (i < n) step(cur, &gl[r * 8], hi, static_cast<uint32_t>(nr), A);
         }
     }
     // no ring DMA may land in the row images (they alias the ring)
@@ -322,8 +335,7 @@ __device__ __forceinline__ void tile_body(const TileArgs &t) {
         acc[4][b] = A.a45[b]; acc[5][b] = A.a45[8 + b];
         acc[6][b] = A.a67[b]; acc[7][b] = A.a67[8 + b];
     }
-    const int nr = min(8, t.nrows - 8 * part);
-    store_rows<0>(sink, nr, 8 * part, acc);
+    store_rows<0>(sink, nr, y0, acc);
 }
 
 #define SH_TILE_KERNEL(P, CW)                                                                      \
@@ -333,21 +345,13 @@ __device__ __forceinline__ void tile_body(const TileArgs &t) {
     __global__ __launch_bounds__(64 * CW * P) void tile_dec_p##P(TileArgs t) {                    \
         tile_body<TShape<P, CW>, true>(t);                                                        \
     }
+// Part counts whose workgroups fill the CU's 4 SIMDs evenly (P * CW a multiple of 4; tile_parts)
 SH_TILE_KERNEL(1, 4)
 SH_TILE_KERNEL(2, 4)
-SH_TILE_KERNEL(3, 2)
 SH_TILE_KERNEL(4, 2)
-SH_TILE_KERNEL(5, 2)
 SH_TILE_KERNEL(6, 2)
-SH_TILE_KERNEL(7, 2)
 SH_TILE_KERNEL(8, 2)
-SH_TILE_KERNEL(9, 1)
-SH_TILE_KERNEL(10, 1)
-SH_TILE_KERNEL(11, 1)
 SH_TILE_KERNEL(12, 1)
-SH_TILE_KERNEL(13, 1)
-SH_TILE_KERNEL(14, 1)
-SH_TILE_KERNEL(15, 1)
 SH_TILE_KERNEL(16, 1)
 
 template <int P, int CW>
@@ -366,11 +370,21 @@ hipError_t launch_p(const TileArgs &t0, bool dec, hipStream_t s, void (*ke)(Tile
 
 }  // namespace tile
 
+// Parts (part-waves per column-wave) for a launch of nrows <= 128 output rows: the smallest
+// balanced count with <= 8 rows per part. A workgroup whose wave count is not a multiple of the
+// CU's 4 SIMDs leaves one SIMD with an extra wave of every workgroup (10 waves at (150,40):
+// 3, 3, 2, 2); parts then hold 4..8 rows and skip their unused snippet calls.
+int tile_parts(int nrows) {
+    const int p0 = (nrows + 7) / 8;
+    for (int p : {1, 2, 4, 6, 8, 12, 16})
+        if (p >= p0) return p;
+    return 0;
+}
+
 int tile_steps_per_group(int parts) {
     switch (parts) {
 #define SH_S(P, CW) case P: return tile::TShape<P, CW>::S;
-        SH_S(1, 4) SH_S(2, 4) SH_S(3, 2) SH_S(4, 2) SH_S(5, 2) SH_S(6, 2) SH_S(7, 2) SH_S(8, 2)
-        SH_S(9, 1) SH_S(10, 1) SH_S(11, 1) SH_S(12, 1) SH_S(13, 1) SH_S(14, 1) SH_S(15, 1) SH_S(16, 1)
+        SH_S(1, 4) SH_S(2, 4) SH_S(4, 2) SH_S(6, 2) SH_S(8, 2) SH_S(12, 1) SH_S(16, 1)
 #undef SH_S
     }
     return 0;
@@ -381,12 +395,10 @@ bool tile_ok(int B) { return B % 8 == 0 && B / 8 >= 16; }
 hipError_t launch_tile(const TileArgs &t, bool dec, hipStream_t s) {
     if (t.f.groups <= 0 || t.nrows <= 0) return hipSuccess;
     if (!tile_ok(t.f.geo.B)) return hipErrorNotSupported;
-    const int parts = (t.nrows + 7) / 8;
-    switch (parts) {
+    switch (tile_parts(t.nrows)) {
 #define SH_L(P, CW) \
     case P: return tile::launch_p<P, CW>(t, dec, s, tile::tile_enc_p##P, tile::tile_dec_p##P);
-        SH_L(1, 4) SH_L(2, 4) SH_L(3, 2) SH_L(4, 2) SH_L(5, 2) SH_L(6, 2) SH_L(7, 2) SH_L(8, 2)
-        SH_L(9, 1) SH_L(10, 1) SH_L(11, 1) SH_L(12, 1) SH_L(13, 1) SH_L(14, 1) SH_L(15, 1) SH_L(16, 1)
+        SH_L(1, 4) SH_L(2, 4) SH_L(4, 2) SH_L(6, 2) SH_L(8, 2) SH_L(12, 1) SH_L(16, 1)
 #undef SH_L
     }
     return hipErrorNotSupported;

@@ -216,12 +216,14 @@ def test_decode_batch_roundtrip_and_oracle(sh, k, m, B, G, e_fixed):
         assert np.array_equal(np.stack(b), blocks[g].cpu().numpy())
 
 
-# Off-grid (k, m): the runtime-coefficient tile kernels (csrc/tile_snip.hip) -- one part (m <= 8),
-# 2..8 parts (two column-waves), 9..16 parts (one column-wave), two launches (m > 128), the
-# shapes Shorthair's policy issues between the compiled pairs, and odd group counts (partial tiles).
+# Off-grid (k, m): the runtime-coefficient tile kernels (csrc/tile_snip.hip) -- every part count
+# (tile_parts: 1, 2, 4, 6, 8, 12, 16 parts of 4..8 rows; m = 3, 10, 24, 40, 60, 76, 100), two
+# launches (m > 128), the shapes Shorthair's policy issues between the compiled pairs, and odd group
+# counts (partial tiles).
 TILE_SHAPES = [(120, 136, 1400, 37), (150, 40, 1400, 301), (50, 10, 1000, 513), (180, 76, 1352, 45),
                (2, 254, 128, 61), (100, 100, 200, 77), (5, 3, 128, 999), (70, 72, 520, 130),
-               (17, 5, 1352, 9), (60, 24, 4104, 11), (33, 33, 136, 257), (240, 16, 264, 40)]
+               (17, 5, 1352, 9), (60, 24, 4104, 11), (33, 33, 136, 257), (240, 16, 264, 40),
+               (150, 60, 1400, 33), (90, 49, 512, 70)]
 
 
 @pytest.mark.parametrize("k,m,B,G", TILE_SHAPES)

@@ -226,24 +226,33 @@ class Body:
 
 
 def shape(k, m):
-    """(P parts, CW column waves, R ring slots, waves/SIMD the registers are allocated for).
+    """(P parts, CW column waves, R ring slots, waves/SIMD the registers are allocated for, S).
     <= ROWS_PER_PART rows per part (8 rows = 64 accumulator VGPRs: ~100 VGPRs, 4 waves/SIMD; the
-    window tables are rebuilt per part, +22 ops per part and step), 4 waves per workgroup."""
+    window tables are rebuilt per part, +22 ops per part and step).
+    A workgroup's wave count must be a multiple of the CU's 4 SIMDs: otherwise one SIMD carries an
+    extra wave of every workgroup and paces it. So P in {1, 2, 4} with CW = 8 / P (8 waves, two
+    workgroups per CU); any other P becomes 8 parts of <= 9 rows with CW = 2 (16 waves, one
+    workgroup per CU with a 128 KB ring): (190,66,1336) encode 0.919 vs 1.266 ms and stage A 1.034
+    vs 1.335 ms against 9 one-column-wave parts (9 waves, one workgroup per CU); (200,56,1352)
+    0.883 vs 0.957 / 0.967 vs 1.000 ms against 7 parts (7 waves)."""
     P = (m + ROWS_PER_PART - 1) // ROWS_PER_PART
-    # Up to 16 waves per workgroup: the CW waves of one part run the SAME straight-line code in
-    # lockstep (one barrier per step), so they share every instruction-cache line they fetch.
-    # (With one wave per part the code stream -- ~0.7 KB per step and part -- outweighs the data
-    # stream and instruction fetch, not HBM, bounds the kernel.)
-    CW = int(os.environ.get("SH_CW", str(max(1, min(8, 8 // P)))))
-    # LDS per workgroup (2 per CU): ring of R slots, <= ~76 KB (the 2 KB per wave of store
-    # scratch aliases the ring after the last step)
-    nw = CW * P
-    slot = 8 * CW * 64 * 4
-    rmax = int(os.environ.get("SH_RING_MAX", "19"))
     rbytes = int(os.environ.get("SH_RING_BYTES", "65536"))  # > 64 KB: with -DSH_RING_LIMIT (experiments)
-    R = int(os.environ.get("SH_RING", str(max(3, min(rmax, rbytes // slot, (76 * 1024) // slot)))))
+    minw_default = None
+    if "SH_CW" not in os.environ and P not in (1, 2, 4):
+        if m > 72:
+            raise ValueError(f"no balanced part layout for m={m} (at most 8 parts of 9 rows)")
+        P, CW, rbytes, minw_default = 8, 2, 131072, "4"
+    else:
+        # Up to 16 waves per workgroup: the CW waves of one part run the SAME straight-line code in
+        # lockstep (one barrier per step), so they share every instruction-cache line they fetch.
+        CW = int(os.environ.get("SH_CW", str(max(1, min(8, 8 // P)))))
+    # LDS per workgroup: ring of R slots (the 2 KB per wave of store scratch aliases the ring after
+    # the last step)
+    slot = 8 * CW * 64 * 4
+    rmax = int(os.environ.get("SH_RING_MAX", "19" if rbytes <= 65536 else "16"))
+    R = int(os.environ.get("SH_RING", str(max(3, min(rmax, rbytes // slot, max(76 * 1024, rbytes) // slot)))))
     rows = (m + P - 1) // P
-    minw = int(os.environ.get("SH_MIN_WAVES", "2" if rows > 12 else ("3" if rows > 8 else "4")))
+    minw = int(os.environ.get("SH_MIN_WAVES", minw_default or ("2" if rows > 12 else ("3" if rows > 8 else "4"))))
     # blocks per barrier: R >= 2*SYNC + 1 keeps >= 1 group of DMA in flight past the one waited for
     sync = int(os.environ.get("SH_SYNC", str(max(1, min(4, (R - 1) // 2 - 1)))))
     return P, CW, R, minw, sync
