@@ -446,7 +446,8 @@ struct DecodeWS {
 bool stageb_v2_on(const sh::Geometry &geo, int emax) {
     static const bool old = std::getenv("SH_STAGEB_OLD") != nullptr;
     static const int vmax = std::getenv("SH_V2_MAX") ? std::atoi(std::getenv("SH_V2_MAX")) : 128;  // measurement
-    return !old && emax > 16 && emax <= vmax && sh::stageb_v2_ok(geo, emax);
+    static const int vmin = std::getenv("SH_V2_MIN") ? std::atoi(std::getenv("SH_V2_MIN")) : 16;   // measurement
+    return !old && emax > vmin && emax <= vmax && sh::stageb_v2_ok(geo, emax);
 }
 
 size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool need_recovered) {

@@ -236,32 +236,57 @@ __device__ __forceinline__ int mod255(int v) {
     return v < 0 ? v + 255 : v;
 }
 
-__global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
-    const int g = blockIdx.x;
-    const int lane = threadIdx.x;
+// Per-wave scratch of decode_setup (one group per wave).
+struct SetupScratch {
+    uint8_t rows[256];
+    uint32_t present[64];  // occurrences of each row value, 4 x 8-bit counts per word
+    uint8_t rec[256];      // array index of the i-th recovery block
+    uint8_t rrow[256];     // its generator row r_i = row - k
+    uint8_t era[256];      // j-th erased original row E_j
+    uint8_t x[256], y[256];
+    uint8_t la[256], lb[256], lx[256];  // logs mod 255
+};
+
+// Every wave handles its own group and synchronises only with itself: its lanes run in lockstep,
+// so its LDS writes are visible to all of its lanes once they completed (lgkmcnt(0)).
+#define SH_WAVE_SYNC() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+
+// W groups per workgroup (one wave each): the exp/log tables are staged once per workgroup
+// ((28,4,256), 209,263 groups: one wave per workgroup spent 0.28 ms of a 0.81 ms decode).
+template <int W>
+__global__ __launch_bounds__(64 * W, 8) void decode_setup(DecodeSetupArgs a, int groups) {
+    const int wave = threadIdx.x >> 6;
+    const int g = blockIdx.x * W + wave;
+    const int lane = threadIdx.x & 63;
     const int k = a.k, m = a.m;
     __shared__ uint8_t s_exp[512];
     __shared__ uint8_t s_log[256];
-    __shared__ uint8_t s_rows[256];
-    __shared__ uint32_t s_present[64];  // occurrences of each row value, 4 x 8-bit counts per word
-    __shared__ uint8_t s_rec[256];      // array index of the i-th recovery block
-    __shared__ uint8_t s_rrow[256];     // its generator row r_i = row - k
-    __shared__ uint8_t s_era[256];      // j-th erased original row E_j
-    __shared__ uint8_t s_x[256], s_y[256];
-    __shared__ uint8_t s_la[256], s_lb[256], s_lx[256];  // logs mod 255 (~3.4 KB in all: 32 waves/CU)
-    __shared__ uint8_t s_gj[6 * 12];    // [S | I] for the m <= 6 Gauss-Jordan
-    __shared__ int s_piv;
+    // generator data the coefficients need, staged with the tables so the per-group chain has one
+    // global round trip (the rows): m <= 6 the searched rows 1..m-1, m >= 7 the Cauchy X', Y'
+    __shared__ uint8_t s_gen[5 * 256];
+    __shared__ uint8_t s_xp[256], s_yp[256];
+    __shared__ SetupScratch sw[W];
+    SetupScratch &S = sw[wave];
 
-    for (int i = lane; i < 512; i += 64) s_exp[i] = a.gf_exp[i];
-    for (int i = lane; i < 256; i += 64) s_log[i] = static_cast<uint8_t>(a.gf_log[i]);
-    s_present[lane] = 0;
-    auto present = [&](int r) { return static_cast<int>((s_present[r >> 2] >> (8 * (r & 3))) & 0xFFu); };
-    const uint8_t *rows = a.rows + static_cast<long long>(g) * a.rows_gstride;
-    for (int j = lane; j < k; j += 64) s_rows[j] = rows[j];
-    __syncthreads();
+    if (g < groups) {
+        const uint8_t *rows = a.rows + static_cast<long long>(g) * a.rows_gstride;
+        for (int j = lane; j < k; j += 64) S.rows[j] = rows[j];
+    }
+    S.present[lane] = 0;
+    for (int i = threadIdx.x; i < 512; i += 64 * W) s_exp[i] = a.gf_exp[i];
+    for (int i = threadIdx.x; i < 256; i += 64 * W) s_log[i] = static_cast<uint8_t>(a.gf_log[i]);
+    if (m <= 6) {
+        for (int i = threadIdx.x; i < (m - 1) * k; i += 64 * W) s_gen[i] = a.gen[i];
+    } else {
+        for (int i = threadIdx.x; i < k; i += 64 * W) s_xp[i] = a.xp[i];
+        for (int i = threadIdx.x; i < m; i += 64 * W) s_yp[i] = a.yp[i];
+    }
+    __syncthreads();  // the only workgroup barrier: waves below may return independently
+    if (g >= groups) return;
+    auto present = [&](int r) { return static_cast<int>((S.present[r >> 2] >> (8 * (r & 3))) & 0xFFu); };
     for (int j = lane; j < k; j += 64)  // a row occurs at most k <= 255 times: no carry between counts
-        atomicAdd(&s_present[s_rows[j] >> 2], 1u << (8 * (s_rows[j] & 3)));
-    __syncthreads();
+        atomicAdd(&S.present[S.rows[j] >> 2], 1u << (8 * (S.rows[j] & 3)));
+    SH_WAVE_SYNC();
     // A row listed twice, or a recovery row past the generator (row >= k + m), is outside the
     // reference's contract (it would decode garbage): the group is left untouched and reported.
     bool bad = false;
@@ -278,12 +303,12 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
     int nrec = 0;
     for (int base = 0; base < k; base += 64) {
         const int j = base + lane;
-        const bool isrec = (j < k) && (s_rows[j] >= k);
+        const bool isrec = (j < k) && (S.rows[j] >= k);
         const unsigned long long mask = __ballot(isrec);
         if (isrec) {
             const int pos = nrec + __popcll(mask & ((1ull << lane) - 1ull));
-            s_rec[pos] = static_cast<uint8_t>(j);
-            s_rrow[pos] = static_cast<uint8_t>(s_rows[j] - k);
+            S.rec[pos] = static_cast<uint8_t>(j);
+            S.rrow[pos] = static_cast<uint8_t>(S.rows[j] - k);
         }
         nrec += __popcll(mask);
     }
@@ -294,11 +319,11 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
         const unsigned long long mask = __ballot(miss);
         if (miss) {
             const int pos = nera + __popcll(mask & ((1ull << lane) - 1ull));
-            s_era[pos] = static_cast<uint8_t>(x);
+            S.era[pos] = static_cast<uint8_t>(x);
         }
         nera += __popcll(mask);
     }
-    __syncthreads();
+    SH_WAVE_SYNC();
     const int e = nrec;
     if (lane == 0) a.e_out[g] = e;
     const bool fixed_mode = (a.coefA == nullptr);
@@ -309,7 +334,7 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
         for (int x = lane; x < KP; x += 64) pos[x] = 0xFF;
         for (int y = lane; y < MP; y += 64) rpos[y] = 0xFF;
         for (int j = lane; j < k; j += 64) {  // same wave, issued after the fills: ordered
-            const int row = s_rows[j];
+            const int row = S.rows[j];
             if (row < k) pos[row] = static_cast<uint8_t>(j);
             else if (row - k < m) rpos[row - k] = static_cast<uint8_t>(j);
         }
@@ -326,23 +351,23 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
     uint8_t *rec_idx = a.rec_idx + static_cast<long long>(g) * emax;
     uint8_t *era = a.erasures + static_cast<long long>(g) * emax;
     for (int i = lane; i < e; i += 64) {
-        rec_idx[i] = s_rec[i];
-        era[i] = s_era[i];
+        rec_idx[i] = S.rec[i];
+        era[i] = S.era[i];
     }
     auto C = [&](int r, int x) -> uint32_t {
-        return r == 0 ? 1u : a.gen[static_cast<long long>(r - 1) * k + x];
+        return r == 0 ? 1u : (m <= 6 ? s_gen[(r - 1) * k + x] : a.gen[static_cast<long long>(r - 1) * k + x]);
     };
 
     // Stage-A coefficients (generic path only), row-major [i][j], leading dimension ldA.
     if (!fixed_mode) {
         uint8_t *A = a.coefA + static_cast<long long>(g) * a.coefA_gstride;
         for (int i = 0; i < e; ++i) {
-            const int r = s_rrow[i];
+            const int r = S.rrow[i];
             for (int j = lane; j < a.ldA; j += 64) {
                 uint32_t c = 0;
                 if (j < k) {
-                    const int row = s_rows[j];
-                    c = row < k ? C(r, row) : (j == s_rec[i] ? 1u : 0u);
+                    const int row = S.rows[j];
+                    c = row < k ? C(r, row) : (j == S.rec[i] ? 1u : 0u);
                 }
                 A[static_cast<long long>(i) * a.ldA + j] = static_cast<uint8_t>(c);
             }
@@ -361,7 +386,7 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
     const uint64_t tnull = a.snip_base + static_cast<uint64_t>(SNIP_NULL) * SNIP_STRIDE;
     if (fixed_mode) {
         uint8_t *rr = a.rrow + static_cast<long long>(g) * a.ldR;
-        for (int i = lane; i < e; i += 64) rr[i] = s_rrow[i];
+        for (int i = lane; i < e; i += 64) rr[i] = S.rrow[i];
     }
     // Every entry stage B reads is written exactly once: the coefficient of (i < e, j < e), the
     // null snippet / zero for the unused outputs j in [e, ldB), and zero rows i >= e (bytes only).
@@ -385,28 +410,28 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
     };
     if (m >= 7) {
         for (int t = lane; t < e; t += 64) {
-            s_x[t] = a.xp[s_era[t]];
-            s_y[t] = a.yp[s_rrow[t]];
+            S.x[t] = s_xp[S.era[t]];
+            S.y[t] = s_yp[S.rrow[t]];
         }
-        __syncthreads();
+        SH_WAVE_SYNC();
         for (int t = lane; t < e; t += 64) {
-            const int xt = s_x[t], yt = s_y[t];
+            const int xt = S.x[t], yt = S.y[t];
             int la = 0, lb = 0;
             for (int q = 0; q < e; ++q) {
-                la += s_log[xt ^ s_y[q]];
-                lb += s_log[s_x[q] ^ yt];
+                la += s_log[xt ^ S.y[q]];
+                lb += s_log[S.x[q] ^ yt];
                 if (q != t) {
-                    la -= s_log[xt ^ s_x[q]];
-                    lb -= s_log[yt ^ s_y[q]];
+                    la -= s_log[xt ^ S.x[q]];
+                    lb -= s_log[yt ^ S.y[q]];
                 }
             }
-            s_la[t] = static_cast<uint8_t>(mod255(la));
-            s_lb[t] = static_cast<uint8_t>(mod255(lb));
-            s_lx[t] = s_log[xt];
+            S.la[t] = static_cast<uint8_t>(mod255(la));
+            S.lb[t] = static_cast<uint8_t>(mod255(lb));
+            S.lx[t] = s_log[xt];
         }
-        __syncthreads();
+        SH_WAVE_SYNC();
         auto coef = [&](int j, int i) -> uint32_t {
-            return s_exp[mod255(s_la[j] + s_lb[i] - s_lx[j] - s_log[s_x[j] ^ s_y[i]])];
+            return s_exp[mod255(S.la[j] + S.lb[i] - S.lx[j] - s_log[S.x[j] ^ S.y[i]])];
         };
         // Walk the output in memory order so every store instruction writes contiguous bytes,
         // the unused entries included: addresses [j/8][i][j%8] (i < e), bytes [i][j] (i < emax).
@@ -427,55 +452,36 @@ __global__ __launch_bounds__(64) void decode_setup(DecodeSetupArgs a) {
         return;
     }
     fill_unused();  // the Gauss-Jordan below writes the (i < e, j < e) entries with put()
-    // m <= 6: Gauss-Jordan on [S | I] (e <= 5).
+    // m <= 6: Gauss-Jordan on [S | I] (e <= 5), one element per lane (lane = row * 2e + column),
+    // rows exchanged by cross-lane reads: a handful of dependent LDS trips per column instead of
+    // serial pivot scans and an LDS round trip per row.
     const int w = 2 * e;
-    for (int t = lane; t < e * w; t += 64) {
-        const int i = t / w, c = t - i * w;
-        s_gj[i * w + c] = static_cast<uint8_t>(c < e ? C(s_rrow[i], s_era[c]) : (c - e == i ? 1 : 0));
-    }
-    __syncthreads();
+    const int r = lane / w, c = lane - r * w;
+    const bool el = lane < e * w;
+    uint32_t v = 0;
+    if (el) v = c < e ? C(S.rrow[r], S.era[c]) : (c - e == r ? 1u : 0u);
     auto gmul = [&](uint32_t x, uint32_t y) -> uint32_t {
         return (x && y) ? s_exp[s_log[x] + s_log[y]] : 0u;
     };
     for (int col = 0; col < e; ++col) {
-        if (lane == 0) {
-            int p = -1;
-            for (int r = col; r < e; ++r)
-                if (s_gj[r * w + col]) { p = r; break; }
-            s_piv = p;
-        }
-        __syncthreads();
-        const int p = s_piv;
-        if (p < 0) {  // singular: impossible for an MDS submatrix
+        const unsigned long long cand = __ballot(el && c == col && r >= col && v != 0);
+        if (cand == 0ull) {  // singular: impossible for an MDS submatrix
             if (lane == 0) {
                 a.e_out[g] = -1;
                 if (a.errors) atomicAdd(a.errors, 1);
             }
             return;
         }
-        if (lane < w && p != col) {
-            const uint8_t t = s_gj[p * w + lane];
-            s_gj[p * w + lane] = s_gj[col * w + lane];
-            s_gj[col * w + lane] = t;
-        }
-        __syncthreads();
-        const uint32_t pinv = s_exp[255 - s_log[s_gj[col * w + col]]];
-        if (lane < w) s_gj[col * w + lane] = static_cast<uint8_t>(gmul(s_gj[col * w + lane], pinv));
-        __syncthreads();
-        if (lane < w)
-            for (int r = 0; r < e; ++r) {
-                if (r == col) continue;
-                const uint32_t f = s_gj[r * w + col];
-                if (f && lane != col) s_gj[r * w + lane] ^= static_cast<uint8_t>(gmul(f, s_gj[col * w + lane]));
-            }
-        __syncthreads();
-        if (lane < e && lane != col) s_gj[lane * w + col] = 0;
-        __syncthreads();
+        const int p = (__ffsll(static_cast<long long>(cand)) - 1) / w;  // wave-uniform pivot row
+        if (p != col) v = __shfl(v, r == col ? p * w + c : (r == p ? col * w + c : lane));
+        const uint32_t piv = __shfl(v, col * w + col);
+        const uint32_t pinv = s_exp[255 - s_log[piv]];
+        if (r == col) v = gmul(v, pinv);
+        const uint32_t f = __shfl(v, r * w + col);     // this row's entry in the pivot column
+        const uint32_t pc = __shfl(v, col * w + c);    // the pivot row's entry in this column
+        if (el && r != col) v ^= gmul(f, pc);
     }
-    for (int t = lane; t < e * e; t += 64) {
-        const int j = t / e, i = t - j * e;
-        put(j, i, s_gj[j * w + e + i]);
-    }
+    if (el && c >= e) put(r, c - e, v);
 }
 
 // In-place finish of decode: recovered erasure l (dense scratch) goes to the l-th recovery block
@@ -632,7 +638,8 @@ hipError_t launch_copy_first(const uint8_t *in, long long in_gstride, uint8_t *o
 }
 
 hipError_t launch_decode_setup(const DecodeSetupArgs &a, int groups, hipStream_t stream) {
-    hipLaunchKernelGGL(decode_setup, dim3(groups), dim3(64), 0, stream, a);
+    constexpr int W = 4;
+    hipLaunchKernelGGL(decode_setup<W>, dim3((groups + W - 1) / W), dim3(64 * W), 0, stream, a, groups);
     return hipGetLastError();
 }
 

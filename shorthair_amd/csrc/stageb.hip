@@ -569,18 +569,27 @@ __global__ __launch_bounds__(64 * NW) void stageb_v2(StageBV2Args a) {
     const long long gbase = static_cast<long long>(g) * a.in_gstride;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.in + gbase), static_cast<short>(0), static_cast<int>(a.in_gstride), 0x00020000);
-    const int off = wave * 1024 + lane * 16;
-    const int sa = off / 256, cq = (off % 256) / 4;
-    const uint32_t dsrc = (c0 + cq < geo.nq) ? colx_off(c0 + cq, geo.nq, geo.sub) + static_cast<uint32_t>(sa * geo.sub)
-                                             : 0x80000000u;
+    // DMA pieces of a ring row (1 KB each): piece p by wave p; a one-wave workgroup issues both
+    auto piece_src = [&](int p) {
+        const int off = p * 1024 + lane * 16;
+        const int sa = off / 256, cq = (off % 256) / 4;
+        return (c0 + cq < geo.nq) ? colx_off(c0 + cq, geo.nq, geo.sub) + static_cast<uint32_t>(sa * geo.sub)
+                                  : 0x80000000u;
+    };
+    const uint32_t dsrc = piece_src(NW >= 2 ? wave : 0);
+    const uint32_t dsrc1 = NW >= 2 ? 0u : piece_src(1);
     const int elast = e - 1;
     auto issue = [&](int i) {
         if (wave < 2) {
             const int x = min(i, elast);
             const uint32_t w = __builtin_amdgcn_readlane(rrv, x >> 2);
             const uint32_t soff = ((w >> (8 * (x & 3))) & 0xFFu) * static_cast<uint32_t>(geo.B);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(ring + (i % RB_R) * RB_ROW + wave * 1024),
-                                                     16, i < e ? dsrc : 0x80000000u, soff, 0, 0);
+            uint8_t *dst = ring + (i % RB_R) * RB_ROW + wave * 1024;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)dst, 16,
+                                                     i < e ? dsrc : 0x80000000u, soff, 0, 0);
+            if (NW == 1)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(dst + 1024), 16,
+                                                         i < e ? dsrc1 : 0x80000000u, soff, 0, 0);
         }
     };
     u32x16 a01, a23, a45, a67;
@@ -594,7 +603,7 @@ __global__ __launch_bounds__(64 * NW) void stageb_v2(StageBV2Args a) {
         // own DMAs of rows 4ig..4ig+3 landed (RB_R - 2 * RB_S younger ones may be outstanding);
         // the first barrier also publishes the coefficient copies
         if (wave < 2)
-            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(RB_R - 2 * RB_S) : "memory");
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"((RB_R - 2 * RB_S) * (NW == 1 ? 2 : 1)) : "memory");
         else
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #pragma unroll
@@ -648,12 +657,17 @@ hipError_t launch_stageb_v2(const StageBV2Args &a, hipStream_t stream) {
     // 4-wave chunks need fewer wave slots (e = 66: 3 x 4 waves, 9 active, vs 2 x 8 with 7 idle):
     // (200,56,1352) stage B 0.478 vs 0.532 ms (7 waves), (190,66,1336) 0.763 vs 0.838 ms
     // (stageb_fixed), (120,136,1400) 1.772 vs 2.070 ms (4096 groups).
+    // One or two output octets (emax <= 16): one workgroup of as many waves, no idle waves.
     static const int force = std::getenv("SH_V2_NW") ? std::atoi(std::getenv("SH_V2_NW")) : 0;  // measurement
     const int c4 = (octets + 3) / 4, c8 = (octets + 7) / 8;
-    const int nw = force ? force : (8 * c8 <= 4 * c4 ? 8 : 4);
+    const int nw = force ? force : (octets <= 2 ? octets : (8 * c8 <= 4 * c4 ? 8 : 4));
     const int chunks = (octets + nw - 1) / nw;
     dim3 grid(static_cast<unsigned>(ncc) * a.groups, chunks, 1);
-    if (nw == 4)
+    if (nw == 1)
+        hipLaunchKernelGGL(stageb_v2<1>, grid, dim3(64), 0, stream, a);
+    else if (nw == 2)
+        hipLaunchKernelGGL(stageb_v2<2>, grid, dim3(128), 0, stream, a);
+    else if (nw == 4)
         hipLaunchKernelGGL(stageb_v2<4>, grid, dim3(256), 0, stream, a);
     else
         hipLaunchKernelGGL(stageb_v2<8>, grid, dim3(512), 0, stream, a);
