@@ -105,7 +105,7 @@ struct Shape {
     static constexpr int KP = (K + 3) & ~3, MP = (M + 3) & ~3;
     // <= 64 KB: two workgroups per CU, and ds_read's 16-bit offsets reach every slot; the 16-wave
     // shapes (one workgroup per CU) take 128 KB (slot offsets past 64 KB cost an address add)
-    static_assert(R >= 3 && R * SLOT <= (NW >= 16 ? 131072 : 65536), "ring size");
+    static_assert(R >= 3 && R * SLOT <= 131072, "ring size");
 };
 
 // Per-lane geometry shared by the source and the sink.
