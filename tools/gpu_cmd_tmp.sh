@@ -1,5 +1,7 @@
 set -u
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/t.log 2>&1; rc=$?; tail -2 gpurun_out/t.log; [ $rc -eq 0 ] || exit $rc
-for shp in "28 4 256 209263" "112 16 256 52315" "224 32 256 26157" "28 4 1400 38265" "200 32 1400 8192"; do
-  bash tools/gpu_ab_shape.sh $shp main || exit 1
-done
+mkdir -p gpurun_out
+bash tools/gpu_run.sh tests || exit $?
+IFETCH="SQC_ICACHE_REQ SQC_ICACHE_MISSES SQC_TC_INST_REQ SQC_ICACHE_BUSY_CYCLES" PROFDIR=profiles/r03 bash tools/gpu_profile.sh b > gpurun_out/prof_b.out 2>&1 || { tail -5 gpurun_out/prof_b.out; exit 1; }
+tail -3 gpurun_out/prof_b.out
+timeout -k 10 600 python bench.py > gpurun_out/bench_full.json 2> gpurun_out/bench_full.err || { tail -5 gpurun_out/bench_full.err; exit 1; }
+python tools/sweep_table.py gpurun_out/bench_full.json
