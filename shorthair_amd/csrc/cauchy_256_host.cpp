@@ -22,6 +22,7 @@
 #include "../../include/cauchy_256.h"
 #include "../../include/cauchy_256_batch.h"
 #include "cauchy_math.hpp"
+#include "colsnip.h"
 #include "kernels.hpp"
 
 namespace {
@@ -94,6 +95,8 @@ struct TileLaunch {
     int row0, nrows, nsteps;
     long long tstride;
     uint32_t *targets;  // device [parts][tstride]
+    bool col;           // column snippets (2 dwords per step) instead of per-row snippets (8)
+    uint32_t hi;        // high dword of every snippet address of the launch
 };
 
 struct Context {
@@ -102,6 +105,8 @@ struct Context {
     int device = 0;
     hipStream_t stream = nullptr;
     uint64_t snip_base = 0;           // stage-B snippet table address (code object)
+    uint64_t col_base[SH_COL_TUS] = {};  // column-snippet tables (csrc/gen/colsnip_<t>.hip)
+    bool col_ok = false;              // ... all inside one 4 GB page (the kernels take low dwords)
     uint64_t *d_rowbytes = nullptr;   // 256 x 8 bytes
     uint8_t *d_exp = nullptr;         // 512
     uint16_t *d_log = nullptr;        // 256
@@ -153,6 +158,19 @@ int init_locked(Context &c, int device) {
     SH_CHECK(hipMalloc(&c.d_log, 512));
     SH_CHECK(hipMemcpy(c.d_log, f.log, 512, hipMemcpyHostToDevice));
     SH_CHECK(sh::stageb_snip_base(&c.snip_base, c.stream));
+    SH_CHECK(sh::colsnip_bases(c.col_base, SH_COL_TUS, c.stream));
+    {
+        // every column-snippet address must share one high dword and have a non-zero low dword
+        // (0 means "no call" to the kernels)
+        const uint64_t hi0 = c.col_base[0] >> 32;
+        bool ok = true;
+        for (int t = 0; t < SH_COL_TUS; ++t) {
+            const uint64_t n = static_cast<uint64_t>(SH_COL_BLOCKS_PER_TU) * 256 + (t == 0 ? 9 : 0);
+            const uint64_t lo = c.col_base[t], hi = lo + n * SH_COL_STRIDE;
+            ok = ok && (lo >> 32) == hi0 && (hi >> 32) == hi0 && static_cast<uint32_t>(lo) != 0;
+        }
+        c.col_ok = ok;
+    }
     c.device = device;
     c.ready = true;
     return 0;
@@ -266,27 +284,70 @@ const std::vector<TileLaunch> *tile_plan(Context &c, int k, int m, bool dec) {
     const std::vector<uint8_t> G = sh::generator_matrix(k, m);  // [m][k], row 0 = ones
     const uint32_t base = static_cast<uint32_t>(c.snip_base);
     auto addr = [&](int cf) { return base + static_cast<uint32_t>(cf ? cf : sh::SNIP_NULL) * sh::SNIP_STRIDE; };
+    // Decode stage A at m >= 7 runs column snippets (csrc/gen/colsnip_<t>.hip: one call per 4
+    // rows, addressed by the input's Cauchy parameter X'_x, as the rows' Y' are the same for every
+    // m; no VGPR-index mode): (150,40) 1.231 vs 1.317 ms, (180,76) 2.72 vs 2.82, (120,136) 3.83 vs
+    // 4.37, (90,49) 0.98 vs 1.12 against the per-row snippets. Encode keeps the per-row snippets
+    // ((180,76) 2.30 vs 2.43 ms; the others within 5 %): a column snippet's table (16 KB per
+    // generator row) misses the instruction cache where the 18 KB per-row table stays resident.
+    // SH_NO_COL / SH_COL_ENC: measurement switches.
+    static const bool no_col = std::getenv("SH_NO_COL") != nullptr;
+    static const bool col_enc = std::getenv("SH_COL_ENC") != nullptr;
+    const bool col = m >= 7 && c.col_ok && !no_col && (dec || col_enc);
+    std::vector<uint8_t> xp, yp;
+    if (col) sh::cauchy_params(k, m, xp, yp);
+    auto col_addr = [&](int blk, int v) {  // block = 4 generator rows
+        const int tu = blk / SH_COL_BLOCKS_PER_TU, loc = blk - tu * SH_COL_BLOCKS_PER_TU;
+        return static_cast<uint32_t>(c.col_base[tu] + (static_cast<uint64_t>(loc) * 256 + v) * SH_COL_STRIDE);
+    };
     std::vector<TileLaunch> plan;
     for (int row0 = 0; row0 < m; row0 += 128) {
         TileLaunch L{};
         L.row0 = row0;
         L.nrows = std::min(128, m - row0);
         L.nsteps = k + (dec ? L.nrows : 0);
+        L.col = col;
+        L.hi = static_cast<uint32_t>((col ? c.col_base[0] : c.snip_base) >> 32);
         const int parts = sh::tile_parts(L.nrows);
         const int S = sh::tile_steps_per_group(parts);
-        L.tstride = static_cast<long long>((L.nsteps + S - 1) / S) * S * 8;
+        const int per = col ? 2 : 8;
+        L.tstride = static_cast<long long>((L.nsteps + S - 1) / S) * S * per;
         // + 128 dwords of slack: a step slice's last scalar loads may run up to S - 1 steps past
         // the part's table (into the next part's, or this slack after the last)
-        std::vector<uint32_t> t(static_cast<size_t>(parts) * L.tstride + 128, addr(0));
-        for (int p = 0; p < parts; ++p)
-            for (int x = 0; x < L.nsteps; ++x)
-                for (int j = 0; j < 8; ++j) {
-                    // part p: rows [p * nrows / parts, (p + 1) * nrows / parts) (tile_snip.hip)
-                    const int yy = p * L.nrows / parts + j;
-                    if (yy >= (p + 1) * L.nrows / parts) continue;
-                    const int cf = x < k ? G[static_cast<size_t>(row0 + yy) * k + x] : (x - k == yy ? 1 : 0);
-                    t[static_cast<size_t>(p) * L.tstride + static_cast<size_t>(x) * 8 + j] = addr(cf);
+        std::vector<uint32_t> t(static_cast<size_t>(parts) * L.tstride + 128, 0u);  // 0: no call
+        const int nb4 = (L.nrows + 3) / 4;
+        for (int p = 0; p < parts; ++p) {
+            if (col) {
+                // part p: 4-row blocks [b0, b1) (one or two; tile_snip.hip computes the same)
+                const int b0 = p * nb4 / parts, b1 = (p + 1) * nb4 / parts;
+                const int yend = std::min(4 * b1, L.nrows);
+                for (int x = 0; x < L.nsteps; ++x) {
+                    uint32_t *e = &t[static_cast<size_t>(p) * L.tstride + static_cast<size_t>(x) * 2];
+                    if (x < k) {
+                        for (int i = 0; i < b1 - b0; ++i) e[i] = col_addr(row0 / 4 + b0 + i, xp[x]);
+                    } else {
+                        const int yy = x - k;  // decode: recovery row yy into its residual row
+                        if (yy >= 4 * b0 && yy < yend)
+                            e[0] = static_cast<uint32_t>(c.col_base[0] + SH_COL_UNIT((yy - 4 * b0 + 4 * (b0 & 1)) & 7));
+                    }
                 }
+                continue;
+            }
+            // part p: rows [p * nrows / parts, (p + 1) * nrows / parts) (tile_snip.hip)
+            const int y0 = p * L.nrows / parts, y1 = (p + 1) * L.nrows / parts;
+            for (int x = 0; x < L.nsteps; ++x) {
+                uint32_t *e = &t[static_cast<size_t>(p) * L.tstride + static_cast<size_t>(x) * 8];
+                if (x >= k) {  // decode recovery-row step: the unit snippet on its row, no other call
+                    const int yy = x - k;
+                    if (yy >= y0 && yy < y1) e[yy - y0] = addr(1);
+                    continue;
+                }
+                for (int j = 0; j < y1 - y0; ++j) {  // zero coefficient: no call
+                    const int cf = G[static_cast<size_t>(row0 + y0 + j) * k + x];
+                    e[j] = cf ? addr(cf) : 0u;
+                }
+            }
+        }
         if (hipMalloc(&L.targets, t.size() * sizeof(uint32_t)) != hipSuccess) return nullptr;
         if (hipMemcpy(L.targets, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess)
             return nullptr;
@@ -347,7 +408,8 @@ int launch_tile_batch(Context &c, int k, int m, int B, int groups, const uint8_t
         t.f.rpos = rpos;
         t.targets = L.targets;
         t.tstride = L.tstride;
-        t.snip_hi = static_cast<uint32_t>(c.snip_base >> 32);
+        t.snip_hi = L.hi;
+        t.col = L.col ? 1 : 0;
         t.k = k;
         t.m = m;
         t.row0 = L.row0;

@@ -167,7 +167,12 @@ struct TileArgs {
     // slice_steps = 0: one slice over every step.
     int slice_steps, slices;
     long long out_slice_bytes;
+    // Column mode (m >= 7): targets hold 2 dwords per (part, step) -- the column snippets of the
+    // part's one or two 4-row blocks (0 = no call) -- instead of 8 per-row snippet addresses.
+    int col;
 };
+// Base addresses of the column-snippet tables (csrc/gen/colsnip_<t>.hip), one per translation unit.
+hipError_t colsnip_bases(uint64_t *out_host, int n, hipStream_t stream);
 bool tile_ok(int B);
 int tile_parts(int nrows);
 int tile_steps_per_group(int parts);

@@ -138,10 +138,16 @@ struct TSrc {
 };
 
 // One step of a part-wave: window tables of the step's 8 words into v[96:127] (v96 = v112 = 0
-// are the zero entries), then one snippet call per row of the part (nr, 4..8: calls 4..7 are
-// skipped past the part's last row), call j in VGPR-index mode with M0 = 8j so the snippet's
-// destination and first source are accumulator set j (v[32+8j .. 32+8j+7]).
+// are the zero entries), then one snippet call per row of the part, call j in VGPR-index mode
+// with M0 = 8j so the snippet's destination and first source are accumulator set j
+// (v[32+8j .. 32+8j+7]). A zero address skips the call (two SALU): rows past the part's last,
+// zero coefficients, and decode's recovery-row steps, which add the received block into one row
+// of one part (the unit snippet) and call nothing elsewhere.
 #define SH_TILE_STEP_ASM                                                                          \
+    SH_TILE_TABLE_ASM                                                                             \
+    SH_TILE_CALLS_ASM
+
+#define SH_TILE_TABLE_ASM                                                                         \
     "v_mov_b32 v97, %[d0]\n"                                                                      \
     "v_mov_b32 v98, %[d1]\n"                                                                      \
     "v_mov_b32 v100, %[d2]\n"                                                                     \
@@ -171,41 +177,58 @@ struct TSrc {
     "v_xor_b32 v110, v102, %[d3]\n"                                                               \
     "v_xor_b32 v126, v118, %[d7]\n"                                                               \
     "v_xor_b32 v111, v103, %[d3]\n"                                                               \
-    "v_xor_b32 v127, v119, %[d7]\n"                                                               \
+    "v_xor_b32 v127, v119, %[d7]\n"
+
+#define SH_TILE_CALLS_ASM                                                                         \
     "s_mov_b32 s43, %[hi]\n"                                                                      \
     "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"                                                     \
+    "s_cmp_eq_u32 %[g0], 0\n"                                                                     \
+    "s_cbranch_scc1 1f\n"                                                                         \
     "s_mov_b32 s42, %[g0]\n"                                                                      \
     "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
+    "1:\n"                                                                                        \
     "s_set_gpr_idx_idx 8\n"                                                                       \
+    "s_cmp_eq_u32 %[g1], 0\n"                                                                     \
+    "s_cbranch_scc1 2f\n"                                                                         \
     "s_mov_b32 s42, %[g1]\n"                                                                      \
     "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
+    "2:\n"                                                                                        \
     "s_set_gpr_idx_idx 16\n"                                                                      \
+    "s_cmp_eq_u32 %[g2], 0\n"                                                                     \
+    "s_cbranch_scc1 3f\n"                                                                         \
     "s_mov_b32 s42, %[g2]\n"                                                                      \
     "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
+    "3:\n"                                                                                        \
     "s_set_gpr_idx_idx 24\n"                                                                      \
+    "s_cmp_eq_u32 %[g3], 0\n"                                                                     \
+    "s_cbranch_scc1 4f\n"                                                                         \
     "s_mov_b32 s42, %[g3]\n"                                                                      \
     "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
-    "s_cmp_le_u32 %[nr], 4\n"                                                                     \
-    "s_cbranch_scc1 9f\n"                                                         \
+    "4:\n"                                                                                        \
     "s_set_gpr_idx_idx 32\n"                                                                      \
+    "s_cmp_eq_u32 %[g4], 0\n"                                                                     \
+    "s_cbranch_scc1 5f\n"                                                                         \
     "s_mov_b32 s42, %[g4]\n"                                                                      \
     "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
-    "s_cmp_le_u32 %[nr], 5\n"                                                                     \
-    "s_cbranch_scc1 9f\n"                                                         \
+    "5:\n"                                                                                        \
     "s_set_gpr_idx_idx 40\n"                                                                      \
+    "s_cmp_eq_u32 %[g5], 0\n"                                                                     \
+    "s_cbranch_scc1 6f\n"                                                                         \
     "s_mov_b32 s42, %[g5]\n"                                                                      \
     "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
-    "s_cmp_le_u32 %[nr], 6\n"                                                                     \
-    "s_cbranch_scc1 9f\n"                                                         \
+    "6:\n"                                                                                        \
     "s_set_gpr_idx_idx 48\n"                                                                      \
+    "s_cmp_eq_u32 %[g6], 0\n"                                                                     \
+    "s_cbranch_scc1 7f\n"                                                                         \
     "s_mov_b32 s42, %[g6]\n"                                                                      \
     "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
-    "s_cmp_le_u32 %[nr], 7\n"                                                                     \
-    "s_cbranch_scc1 9f\n"                                                         \
+    "7:\n"                                                                                        \
     "s_set_gpr_idx_idx 56\n"                                                                      \
+    "s_cmp_eq_u32 %[g7], 0\n"                                                                     \
+    "s_cbranch_scc1 8f\n"                                                                         \
     "s_mov_b32 s42, %[g7]\n"                                                                      \
     "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
-    "9:\n"                                                                       \
+    "8:\n"                                                                                        \
     "s_set_gpr_idx_off"
 
 struct Acc {
@@ -213,18 +236,47 @@ struct Acc {
     uint32_t z0, z1;
 };
 
-__device__ __forceinline__ void step(const uint32_t (&d)[8], const uint32_t *g, uint32_t hi, uint32_t nr, Acc &A) {
+__device__ __forceinline__ void step(const uint32_t (&d)[8], const uint32_t *g, uint32_t hi, Acc &A) {
     asm volatile(SH_TILE_STEP_ASM
                  : "+{v[32:47]}"(A.a01), "+{v[48:63]}"(A.a23), "+{v[64:79]}"(A.a45), "+{v[80:95]}"(A.a67),
                    "+{v96}"(A.z0), "+{v112}"(A.z1)
                  : [d0] "v"(d[0]), [d1] "v"(d[1]), [d2] "v"(d[2]), [d3] "v"(d[3]), [d4] "v"(d[4]),
                    [d5] "v"(d[5]), [d6] "v"(d[6]), [d7] "v"(d[7]), [g0] "s"(g[0]), [g1] "s"(g[1]),
                    [g2] "s"(g[2]), [g3] "s"(g[3]), [g4] "s"(g[4]), [g5] "s"(g[5]), [g6] "s"(g[6]),
-                   [g7] "s"(g[7]), [hi] "s"(hi), [nr] "s"(nr)
+                   [g7] "s"(g[7]), [hi] "s"(hi)
                  : "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107",
                    "v108", "v109", "v110", "v111", "v113", "v114", "v115", "v116", "v117", "v118", "v119",
                    "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "s40", "s41", "s42",
                    "s43", "m0", "scc", "memory");
+}
+
+// Column-snippet step (m >= 7, csrc/gen/colsnip_*.hip): the same window tables, then one call per
+// 4-row block of the part (g0, g1: snippet-address low dwords; 0 = no call). A column snippet
+// applies all 4 rows' coefficients of the input to its accumulator half with absolute register
+// numbers, so no VGPR-index mode and 1/4 of the calls.
+#define SH_COL_STEP_ASM                                                                           \
+    SH_TILE_TABLE_ASM                                                                             \
+    "s_cmp_eq_u32 %[g0], 0\n"                                                                     \
+    "s_cbranch_scc1 9f\n"                                                                         \
+    "s_mov_b32 s43, %[hi]\n"                                                                      \
+    "s_mov_b32 s42, %[g0]\n"                                                                      \
+    "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
+    "s_cmp_eq_u32 %[g1], 0\n"                                                                     \
+    "s_cbranch_scc1 9f\n"                                                                         \
+    "s_mov_b32 s42, %[g1]\n"                                                                      \
+    "s_swappc_b64 s[40:41], s[42:43]\n"                                                           \
+    "9:\n"
+
+__device__ __forceinline__ void step_col(const uint32_t (&d)[8], uint32_t g0, uint32_t g1, uint32_t hi, Acc &A) {
+    asm volatile(SH_COL_STEP_ASM
+                 : "+{v[32:47]}"(A.a01), "+{v[48:63]}"(A.a23), "+{v[64:79]}"(A.a45), "+{v[80:95]}"(A.a67),
+                   "+{v96}"(A.z0), "+{v112}"(A.z1)
+                 : [d0] "v"(d[0]), [d1] "v"(d[1]), [d2] "v"(d[2]), [d3] "v"(d[3]), [d4] "v"(d[4]),
+                   [d5] "v"(d[5]), [d6] "v"(d[6]), [d7] "v"(d[7]), [g0] "s"(g0), [g1] "s"(g1), [hi] "s"(hi)
+                 : "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107",
+                   "v108", "v109", "v110", "v111", "v113", "v114", "v115", "v116", "v117", "v118", "v119",
+                   "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "s40", "s41", "s42",
+                   "s43", "scc", "memory");
 }
 
 // Every wave joins one barrier per row of a part (8), storing its part's rows < nr.
@@ -239,7 +291,24 @@ __device__ __forceinline__ void store_rows(const Snk &sink, int nr, int y0, cons
     }
 }
 
-template <class S, bool DEC>
+// Column mode: rows of a part are 4-row blocks b0, b0+1 whose accumulator halves follow the
+// block's parity (the column snippets of block r write half r % 2), so row y0 + i lives in
+// accumulator set (i + 4 * (b0 & 1)) % 8.
+template <int ROT, class Snk>
+__device__ __forceinline__ void store_rows_rot(const Snk &sink, int nr, int y0, const uint32_t (&acc)[8][8]) {
+    if constexpr (ROT == 0) {
+        store_rows<0>(sink, nr, y0, acc);
+    } else {
+        uint32_t r[8][8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int b = 0; b < 8; ++b) r[i][b] = acc[(i + ROT) & 7][b];
+        store_rows<0>(sink, nr, y0, r);
+    }
+}
+
+template <class S, bool DEC, bool COL>
 __device__ __forceinline__ void tile_body(const TileArgs &t) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const FixedArgs &a = t.f;
@@ -290,11 +359,15 @@ __device__ __forceinline__ void tile_body(const TileArgs &t) {
 
     // snippet-address low dwords of this part: [ngroups * S steps][8], scalar loads
     typedef const __attribute__((address_space(4))) uint32_t cu32_t;
-    const cu32_t *tp = (const cu32_t *)(t.targets + static_cast<long long>(part) * t.tstride + 8ll * src.x0);
+    constexpr int PER = COL ? 2 : 8;  // snippet-address dwords per step
+    const cu32_t *tp = (const cu32_t *)(t.targets + static_cast<long long>(part) * t.tstride + PER * static_cast<long long>(src.x0));
     const uint32_t hi = t.snip_hi;
-    // this part's rows [y0, y0 + nr): the launch's rows split evenly over the P parts (4..8 each)
-    const int y0 = part * t.nrows / S::P;
-    const int nr = (part + 1) * t.nrows / S::P - y0;
+    // this part's rows [y0, y0 + nr): the launch's rows split evenly over the P parts (4..8 each);
+    // column mode: whole 4-row blocks [b0, b1) (one or two), tile_plan agrees
+    const int nb4 = (t.nrows + 3) / 4;
+    const int b0 = part * nb4 / S::P, b1 = (part + 1) * nb4 / S::P;
+    const int y0 = COL ? 4 * b0 : part * t.nrows / S::P;
+    const int nr = COL ? min(4 * b1, t.nrows) - y0 : (part + 1) * t.nrows / S::P - y0;
 
     Acc A;
 #pragma unroll
@@ -308,9 +381,9 @@ __device__ __forceinline__ void tile_body(const TileArgs &t) {
     uint32_t dA[8], dB[8];
     src.read(0, dA);
     for (int ig = 0; ig < ngroups; ++ig) {
-        uint32_t gl[S::S * 8];
+        uint32_t gl[S::S * PER];
 #pragma unroll
-        for (int j = 0; j < S::S * 8; ++j) gl[j] = tp[ig * S::S * 8 + j];
+        for (int j = 0; j < S::S * PER; ++j) gl[j] = tp[ig * S::S * PER + j];
 #pragma unroll
         for (int r = 0; r < S::S; ++r) {
             const int i = ig * S::S + r;
@@ -322,7 +395,12 @@ __device__ __forceinline__ void tile_body(const TileArgs &t) {
                 for (int u = 0; u < S::S; ++u) src.issue(i + S::R - S::S + u);
             }
             if (i + 1 < n) src.read((i + 1) % S::R, nxt);
-            if (i < n) step(cur, &gl[r * 8], hi, static_cast<uint32_t>(nr), A);
+            if (i < n) {
+                if (COL)
+                    step_col(cur, gl[r * PER], gl[r * PER + 1], hi, A);
+                else
+                    step(cur, &gl[r * PER], hi, A);
+            }
         }
     }
     // no ring DMA may land in the row images (they alias the ring)
@@ -335,15 +413,24 @@ __device__ __forceinline__ void tile_body(const TileArgs &t) {
         acc[4][b] = A.a45[b]; acc[5][b] = A.a45[8 + b];
         acc[6][b] = A.a67[b]; acc[7][b] = A.a67[8 + b];
     }
-    store_rows<0>(sink, nr, y0, acc);
+    if (COL && (b0 & 1))
+        store_rows_rot<4>(sink, nr, y0, acc);
+    else
+        store_rows_rot<0>(sink, nr, y0, acc);
 }
 
 #define SH_TILE_KERNEL(P, CW)                                                                      \
     __global__ __launch_bounds__(64 * CW * P) void tile_enc_p##P(TileArgs t) {                    \
-        tile_body<TShape<P, CW>, false>(t);                                                       \
+        tile_body<TShape<P, CW>, false, false>(t);                                                \
     }                                                                                             \
     __global__ __launch_bounds__(64 * CW * P) void tile_dec_p##P(TileArgs t) {                    \
-        tile_body<TShape<P, CW>, true>(t);                                                        \
+        tile_body<TShape<P, CW>, true, false>(t);                                                 \
+    }                                                                                             \
+    __global__ __launch_bounds__(64 * CW * P) void tile_col_enc_p##P(TileArgs t) {                \
+        tile_body<TShape<P, CW>, false, true>(t);                                                 \
+    }                                                                                             \
+    __global__ __launch_bounds__(64 * CW * P) void tile_col_dec_p##P(TileArgs t) {                \
+        tile_body<TShape<P, CW>, true, true>(t);                                                  \
     }
 // Part counts whose workgroups fill the CU's 4 SIMDs evenly (P * CW a multiple of 4; tile_parts)
 SH_TILE_KERNEL(1, 4)
@@ -381,6 +468,29 @@ int tile_parts(int nrows) {
     return 0;
 }
 
+// The column-snippet tables live in the generated translation units (csrc/gen/colsnip_<t>.hip);
+// each holds its table inside a probe kernel whose only launch reports the table's address.
+__global__ void colsnip_probe_0(uint64_t *out);
+__global__ void colsnip_probe_1(uint64_t *out);
+__global__ void colsnip_probe_2(uint64_t *out);
+__global__ void colsnip_probe_3(uint64_t *out);
+
+hipError_t colsnip_bases(uint64_t *out_host, int n, hipStream_t stream) {
+    if (n != 4) return hipErrorInvalidValue;
+    uint64_t *d = nullptr;
+    hipError_t err = hipMalloc(&d, 4 * sizeof(uint64_t));
+    if (err != hipSuccess) return err;
+    hipLaunchKernelGGL(colsnip_probe_0, dim3(1), dim3(64), 0, stream, d + 0);
+    hipLaunchKernelGGL(colsnip_probe_1, dim3(1), dim3(64), 0, stream, d + 1);
+    hipLaunchKernelGGL(colsnip_probe_2, dim3(1), dim3(64), 0, stream, d + 2);
+    hipLaunchKernelGGL(colsnip_probe_3, dim3(1), dim3(64), 0, stream, d + 3);
+    err = hipGetLastError();
+    if (err == hipSuccess) err = hipMemcpyAsync(out_host, d, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(stream);
+    (void)hipFree(d);
+    return err;
+}
+
 int tile_steps_per_group(int parts) {
     switch (parts) {
 #define SH_S(P, CW) case P: return tile::TShape<P, CW>::S;
@@ -396,8 +506,10 @@ hipError_t launch_tile(const TileArgs &t, bool dec, hipStream_t s) {
     if (t.f.groups <= 0 || t.nrows <= 0) return hipSuccess;
     if (!tile_ok(t.f.geo.B)) return hipErrorNotSupported;
     switch (tile_parts(t.nrows)) {
-#define SH_L(P, CW) \
-    case P: return tile::launch_p<P, CW>(t, dec, s, tile::tile_enc_p##P, tile::tile_dec_p##P);
+#define SH_L(P, CW)                                                                              \
+    case P:                                                                                      \
+        return t.col ? tile::launch_p<P, CW>(t, dec, s, tile::tile_col_enc_p##P, tile::tile_col_dec_p##P) \
+                     : tile::launch_p<P, CW>(t, dec, s, tile::tile_enc_p##P, tile::tile_dec_p##P);
         SH_L(1, 4) SH_L(2, 4) SH_L(4, 2) SH_L(6, 2) SH_L(8, 2) SH_L(12, 1) SH_L(16, 1)
 #undef SH_L
     }

@@ -423,12 +423,103 @@ def gen_snippets():
             f.write("\n".join(t[:5]) + "\n" + " \\\n".join(t[5:]) + "\n")
 
 
+# Column snippets for the runtime-coefficient tile kernels at m >= 7 (csrc/tile_snip.hip). There
+# the generator is C[y][x] = X'_x / (X'_x + Y'_y) with Y'_y = Y[y-1] the SAME for every m (only X'
+# depends on m, cauchy_256.cpp:453-477), so the coefficients of 4 consecutive rows for input x
+# are a function of one byte, v = X'_x. Snippet (block r, v) applies M(C[y][x]) for the rows
+# y = 4r..4r+3 to accumulator sets 4*(r%2)..+3 (v[32+32*(r%2)+8j+b]) from the window tables in
+# v[96:127] (v96 = v112 = 0): 32 v_bitop3_b32 and a return, no VGPR-index mode -- one call per 4
+# rows and input instead of one per row (the index mode alone costs 1.8x).
+# 64 blocks (rows 0..255) x 256 values, COL_STRIDE bytes each, in COL_TUS translation units of
+# COL_BLOCKS_PER_TU blocks; TU 0 also holds 8 "unit" snippets (acc set s ^= the input: decode
+# stage A's recovery-row steps) and a null snippet, at block COL_BLOCKS_PER_TU.
+COL_STRIDE, COL_TUS, COL_BLOCKS_PER_TU = 264, 4, 16
+
+
+def _col_snippet(lines, accs, coefs, label=None):
+    for j, c in enumerate(coefs):
+        v = c
+        for b in range(8):
+            if c:
+                lo, hi = v & 15, v >> 4
+                lines.append(f"v_bitop3_b32 v{accs[j] + b}, v{accs[j] + b}, v{SNIPA_T0 + lo}, v{SNIPA_T1 + hi} bitop3:0x96")
+            v = gmul(v, 2)
+    n = sum(8 for c in coefs if c)
+    lines.append("s_setpc_b64 s[40:41]")
+    lines.append(f".skip {COL_STRIDE - 8 * n - 4}")  # fixed stride (never executed): base + COL_STRIDE * index
+
+
+def gen_colsnips():
+    t = _tables()
+    Y = list(t["Y"]) + [0] * 256
+    inv = [0] + [EXP[(255 - LOG[a]) % 255] for a in range(1, 256)]
+
+    def div(a, b):
+        return 0 if a == 0 or b == 0 else EXP[LOG[a] + 255 - LOG[b]]
+
+    def coef(y, v):
+        return 1 if y == 0 else div(v, v ^ Y[y - 1])
+    for tu in range(COL_TUS):
+        L = []
+        for rl in range(COL_BLOCKS_PER_TU):
+            r = tu * COL_BLOCKS_PER_TU + rl
+            accs = [SNIPA_ACC + 32 * (r % 2) + 8 * j for j in range(4)]
+            for v in range(256):
+                L.append(".p2align 3")
+                _col_snippet(L, accs, [coef(4 * r + j, v) for j in range(4)])
+        if tu == 0:
+            for st in range(8):  # unit snippets: acc set st ^= the input block (coefficient 1)
+                L.append(".p2align 3")
+                _col_snippet(L, [SNIPA_ACC + 8 * st], [1])
+            L.append(".p2align 3")
+            _col_snippet(L, [], [])  # null snippet
+        body = "\n".join(f'    "{l}\\n"' for l in L)
+        src = f"""// GENERATED by tools/gen_fixed_kernels.py -- do not edit. Column snippets, blocks
+// {tu * COL_BLOCKS_PER_TU}..{tu * COL_BLOCKS_PER_TU + COL_BLOCKS_PER_TU - 1} (rows {4 * tu * COL_BLOCKS_PER_TU}..{4 * (tu + 1) * COL_BLOCKS_PER_TU - 1}); see the generator.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+namespace sh {{
+// Holds the table; its only launch reports where the table was loaded.
+__global__ void colsnip_probe_{tu}(uint64_t *out) {{
+    // the table is ~1 MB: jump over it with an absolute (computed) jump, s_branch reaches 128 KB
+    asm volatile("s_getpc_b64 s[42:43]\\n"
+    "s_add_u32 s42, s42, sh_colsnip_end{tu}@rel32@lo+4\\n"
+    "s_addc_u32 s43, s43, sh_colsnip_end{tu}@rel32@hi+12\\n"
+    "s_setpc_b64 s[42:43]\\n"
+    ".p2align 6\\n"
+    "sh_colsnip_base{tu}:\\n"
+{body}
+    "sh_colsnip_end{tu}:\\n" ::: "s42", "s43", "scc", "memory");
+    uint64_t base;
+    asm volatile(
+        "s_getpc_b64 s[42:43]\\n"
+        "s_add_u32 s42, s42, sh_colsnip_base{tu}@rel32@lo+4\\n"
+        "s_addc_u32 s43, s43, sh_colsnip_base{tu}@rel32@hi+12\\n"
+        "s_mov_b64 %0, s[42:43]"
+        : "=s"(base)
+        :
+        : "s42", "s43", "scc");
+    if (threadIdx.x == 0) *out = base;
+}}
+}}  // namespace sh
+"""
+        with open(os.path.join(OUTDIR, f"colsnip_{tu}.hip"), "w") as f:
+            f.write(src)
+    with open(os.path.join(OUTDIR, "colsnip.h"), "w") as f:
+        f.write("// GENERATED by tools/gen_fixed_kernels.py -- column-snippet table layout.\n#pragma once\n"
+                f"#define SH_COL_STRIDE {COL_STRIDE}\n#define SH_COL_TUS {COL_TUS}\n"
+                f"#define SH_COL_BLOCKS_PER_TU {COL_BLOCKS_PER_TU}\n"
+                "#define SH_COL_UNIT(s) ((SH_COL_BLOCKS_PER_TU * 256 + (s)) * SH_COL_STRIDE)  /* offset in TU 0 */\n"
+                "#define SH_COL_NULL ((SH_COL_BLOCKS_PER_TU * 256 + 8) * SH_COL_STRIDE)\n")
+
+
 def main(argv=()):
     cfgs = CONFIGS
     if argv:
         cfgs = [tuple(map(int, a.split(","))) for a in argv]
     paths = [p for (k, m) in cfgs for p in gen_config(k, m)]
     gen_snippets()
+    gen_colsnips()
     # registry of generated shapes
     reg = ["// GENERATED by tools/gen_fixed_kernels.py -- list of compile-time-scheduled (k, m).",
            "#pragma once", "#define SH_FIXED_CONFIGS(X) \\"]

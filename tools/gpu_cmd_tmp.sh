@@ -1,7 +1,6 @@
 set -u
-mkdir -p gpurun_out
-bash tools/gpu_run.sh tests || exit $?
-IFETCH="SQC_ICACHE_REQ SQC_ICACHE_MISSES SQC_TC_INST_REQ SQC_ICACHE_BUSY_CYCLES" PROFDIR=profiles/r03 bash tools/gpu_profile.sh b > gpurun_out/prof_b.out 2>&1 || { tail -5 gpurun_out/prof_b.out; exit 1; }
-tail -3 gpurun_out/prof_b.out
-timeout -k 10 600 python bench.py > gpurun_out/bench_full.json 2> gpurun_out/bench_full.err || { tail -5 gpurun_out/bench_full.err; exit 1; }
-python tools/sweep_table.py gpurun_out/bench_full.json
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_abi.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/t.log 2>&1; rc=$?; tail -2 gpurun_out/t.log; [ $rc -eq 0 ] || exit $rc
+for shp in "150 40 1400 7142" "180 76 1352 6163" "120 136 1400 8928" "90 49 1400 8192" "50 10 1000 30000"; do
+  bash tools/gpu_ab_shape.sh $shp main || exit 1
+  SH_COL_DEC=1 SH_COL_ENC=1 bash tools/gpu_ab_shape.sh $shp main || exit 1
+done
