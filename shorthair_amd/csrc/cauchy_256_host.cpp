@@ -499,16 +499,18 @@ struct DecodeWS {
     long long coefA_gs, coefB_gs;
 };
 
-// Stage B after a full-residual stage A: stageb_v2 for emax > 16, where it measured faster
+// Stage B after a full-residual stage A: stageb_v2 for emax > 8, where it measured faster
 // ((200,32) e = 32: 0.34 vs 0.39 ms; (200,56) e = 56: 0.478 vs 0.532 ms; (190,66) e = 66: 0.763 vs
-// 0.838 ms and (120,136) e = 120: 1.77 vs 2.07 ms against stageb_fixed, with 4- or 8-wave chunks,
-// stageb.hip); round 2's stageb_regs with setup-written snippet addresses for emax <= 16 (C2 decode
-// 0.72 vs 0.79 ms, (28,4,1400) 0.51 vs 0.66 ms). SH_STAGEB_OLD=1 (measurement switch) selects
-// round 2's kernels everywhere; SH_V2_MAX caps the emax served by stageb_v2.
+// 0.838 ms and (120,136) e = 120: 1.77 vs 2.07 ms against stageb_fixed, with 4- or 8-wave chunks;
+// C2 (64,16) e = 16: 0.229 vs 0.280 ms and (112,16) 0.142 vs 0.177 ms against stageb_regs, with
+// 2-wave workgroups and an 8-row ring, stageb.hip); round 2's stageb_regs with setup-written
+// snippet addresses for emax <= 8 ((28,4,1400) 0.114 vs 0.132 ms for a one-wave v2).
+// SH_STAGEB_OLD=1 (measurement switch) selects round 2's kernels everywhere; SH_V2_MIN / SH_V2_MAX
+// bound the emax served by stageb_v2.
 bool stageb_v2_on(const sh::Geometry &geo, int emax) {
     static const bool old = std::getenv("SH_STAGEB_OLD") != nullptr;
     static const int vmax = std::getenv("SH_V2_MAX") ? std::atoi(std::getenv("SH_V2_MAX")) : 128;  // measurement
-    static const int vmin = std::getenv("SH_V2_MIN") ? std::atoi(std::getenv("SH_V2_MIN")) : 16;   // measurement
+    static const int vmin = std::getenv("SH_V2_MIN") ? std::atoi(std::getenv("SH_V2_MIN")) : 8;    // measurement
     return !old && emax > vmin && emax <= vmax && sh::stageb_v2_ok(geo, emax);
 }
 

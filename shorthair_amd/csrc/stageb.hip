@@ -539,10 +539,14 @@ __device__ __forceinline__ void v2_row(const Row8 &d, uint32_t c0, uint32_t c1, 
 
 constexpr int V2_MAXE = 128;  // emax = min(k, m) <= 128 whenever k + m <= 256
 
+// Ring depth: 16 rows (4 per barrier group) for 4- and 8-wave workgroups; 8 rows (2 per group)
+// for the 1- and 2-wave workgroups of emax <= 16, so their 16 KB rings let 9 of them share a CU.
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void stageb_v2(StageBV2Args a) {
+    constexpr int RB_R = NW <= 2 ? 8 : 16, RB_S = RB_R / 4;
+    constexpr int MAXE = NW <= 2 ? 16 : V2_MAXE;  // 1-2 waves: emax <= 16 (launch_stageb_v2)
     __shared__ __attribute__((aligned(16))) uint8_t ring[RB_R * RB_ROW];
-    __shared__ __attribute__((aligned(8))) uint32_t cf[NW][V2_MAXE][2];  // [wave][row] coefficient bytes
+    __shared__ __attribute__((aligned(8))) uint32_t cf[NW][MAXE][2];  // [wave][row] coefficient bytes
     const Geometry geo = a.geo;
     const int ncc = (geo.nq + 63) / 64;
     const int g = blockIdx.x / ncc;
@@ -600,7 +604,7 @@ __global__ __launch_bounds__(64 * NW) void stageb_v2(StageBV2Args a) {
     for (int i = 0; i < RB_R - RB_S; ++i) issue(i);
     const int ngroups = (e + RB_S - 1) / RB_S;
     for (int ig = 0; ig < ngroups; ++ig) {
-        // own DMAs of rows 4ig..4ig+3 landed (RB_R - 2 * RB_S younger ones may be outstanding);
+        // own DMAs of rows RB_S*ig.. landed (RB_R - 2 * RB_S younger ones may be outstanding);
         // the first barrier also publishes the coefficient copies
         if (wave < 2)
             asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"((RB_R - 2 * RB_S) * (NW == 1 ? 2 : 1)) : "memory");
