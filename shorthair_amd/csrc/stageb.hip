@@ -664,7 +664,9 @@ hipError_t launch_stageb_v2(const StageBV2Args &a, hipStream_t stream) {
     // One or two output octets (emax <= 16): one workgroup of as many waves, no idle waves.
     static const int force = std::getenv("SH_V2_NW") ? std::atoi(std::getenv("SH_V2_NW")) : 0;  // measurement
     const int c4 = (octets + 3) / 4, c8 = (octets + 7) / 8;
-    const int nw = force ? force : (octets <= 2 ? octets : (8 * c8 <= 4 * c4 ? 8 : 4));
+    const int nw = (force == 1 || force == 2) && octets <= 2 ? force                       // 1-2 waves hold <= 16 rows
+                   : (force == 4 || force == 8) ? force
+                   : (octets <= 2 ? octets : (8 * c8 <= 4 * c4 ? 8 : 4));
     const int chunks = (octets + nw - 1) / nw;
     dim3 grid(static_cast<unsigned>(ncc) * a.groups, chunks, 1);
     if (nw == 1)
