@@ -449,16 +449,31 @@ def _col_snippet(lines, accs, coefs, label=None):
     lines.append(f".skip {COL_STRIDE - 8 * n - 4}")  # fixed stride (never executed): base + COL_STRIDE * index
 
 
+_COL_Y = None
+
+
+def col_coef(y, v):
+    """Generator coefficient of row y (m >= 7) for an input whose Cauchy parameter X'_x is v:
+    row 0 = ones, else X'/(X' + Y[y-1]) (cauchy_256.cpp:453-477; 0 where the reference's divide
+    would see a zero operand)."""
+    global _COL_Y
+    if _COL_Y is None:
+        _COL_Y = list(_tables()["Y"]) + [0] * 256
+    if y == 0:
+        return 1
+    b = v ^ _COL_Y[y - 1]
+    return 0 if v == 0 or b == 0 else EXP[LOG[v] + 255 - LOG[b]]
+
+
+def cauchy_xp(k, m):
+    """X'_x of the m >= 7 generator (X'_0 = 1, X'_x = X[x-1] at offset n*249 - n(n+1)/2, n = m-7)."""
+    n = m - 7
+    X = _tables()["X"][n * 249 - n * (n + 1) // 2:]
+    return [1] + [X[x - 1] for x in range(1, k)]
+
+
 def gen_colsnips():
-    t = _tables()
-    Y = list(t["Y"]) + [0] * 256
-    inv = [0] + [EXP[(255 - LOG[a]) % 255] for a in range(1, 256)]
-
-    def div(a, b):
-        return 0 if a == 0 or b == 0 else EXP[LOG[a] + 255 - LOG[b]]
-
-    def coef(y, v):
-        return 1 if y == 0 else div(v, v ^ Y[y - 1])
+    coef = col_coef
     for tu in range(COL_TUS):
         L = []
         for rl in range(COL_BLOCKS_PER_TU):
