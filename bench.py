@@ -419,9 +419,14 @@ def _time_ops(args, sh, torch, s, k, m, B, G, data, rec, e_fixed, encode=True, i
     r = {"decode_ms": round(td, 4), "decode_GBps": round(dec_b / td / 1e6, 1),
          "decode_frac": round(dec_b / td / 1e-3 / HBM_PEAK, 4), "mean_e": round(float(es.mean()), 2),
          "decode_ok": ok}
+    # work-normalized rates (picoseconds per group x generator product): the codec's work is
+    # k*m 8x8 products per group for encode and (k*m + e^2) for decode (stage A over all m
+    # rows, stage B e x e), so shapes with more products per byte compare on this column
+    r["decode_ps_per_product"] = round(td * 1e9 / float(G * k * m + (es.astype(np.float64) ** 2).sum()), 2)
     if encode:
         r.update({"encode_ms": round(te, 4), "encode_GBps": round(enc_b / te / 1e6, 1),
-                  "encode_frac": round(enc_b / te / 1e-3 / HBM_PEAK, 4)})
+                  "encode_frac": round(enc_b / te / 1e-3 / HBM_PEAK, 4),
+                  "encode_ps_per_product": round(te * 1e9 / float(G * k * m), 2)})
     return r
 
 
