@@ -13,4 +13,4 @@ for line in open(sys.argv[1]):
         print(f"{s['config']:12s} ({s['k']},{s['m']},{s['B']}) {s['path']:6s} G={s['groups']:6d} "
               f"enc {s.get('encode_ms') or 0:7.4f} ms {s.get('encode_frac') or 0:6.4f}  "
               f"dec {s['decode_ms']:7.4f} ms {s['decode_frac']:6.4f}  e={s['mean_e']}  "
-              f"ps/product enc {s.get('encode_ps_per_product', 0)} dec {s.get('decode_ps_per_product', 0)}")
+              f"product rate enc {s.get('encode_product_rate', 0)} dec {s.get('decode_product_rate', 0)}")
