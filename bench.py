@@ -54,6 +54,8 @@ def parse():
     p.add_argument("--root-steps", type=int, default=3,
                    help="N>1: steps of the root-resident variant (RCCL scatter -> encode -> gather); 0 = skip")
     p.add_argument("--no-sweep", action="store_true", help="skip the C2/C3/C4/Tester-shape leg")
+    p.add_argument("--pg-timeout", type=int, default=120,
+                   help="N>1: torch.distributed collective timeout in seconds (nccl backend)")
     p.add_argument("--backend", default="nccl",
                    help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse the "
                         "multi-rank path with several ranks on one GPU)")
@@ -472,7 +474,11 @@ def main():
     if world > 1:
         torch.cuda.set_device(dev)
         if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+            # a bounded collective timeout: a stuck side leg raises (and is reported) instead of
+            # holding the job past the driver's limit
+            import datetime
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev),
+                                    timeout=datetime.timedelta(seconds=args.pg_timeout))
         else:
             dist.init_process_group(args.backend)
         world = dist.get_world_size()
@@ -558,13 +564,17 @@ def main():
     # ---- root-resident variant (N > 1): groups start and end on rank 0's GPU; one RCCL scatter of
     # the data shards over xGMI, encode on every GPU, one RCCL gather of the recovery shards.
     # Reported beside the main line, never as `value`.
+    # (the main line's last collective runs before the side leg: a failed leg leaves the process
+    # group unusable, and the line must still print)
+    enc_bytes_all = shd.sum_over_ranks(enc_bytes, device="cuda")
     root_res = None
+    pg_ok = True
     if world > 1 and args.root_steps > 0:
         try:
             root_res = root_resident(args, sh, shd, dist, torch, rank, world, G, k, m, B, s, enc_in, enc_out)
         except Exception as exc:  # never lose the main line over the side measurement
             root_res = {"error": f"{type(exc).__name__}: {exc}"}
-    enc_bytes_all = shd.sum_over_ranks(enc_bytes, device="cuda")
+            pg_ok = False
     total = (enc_bytes_all + dec_bytes_all) * args.steps
     value = total / elapsed / 2**30
     ms_per_step = elapsed / args.steps * 1e3
@@ -650,7 +660,11 @@ def main():
                 line["host_path"] = {"error": f"{type(exc).__name__}: {exc}"}
         print(json.dumps(line), flush=True)
     if world > 1:
-        dist.destroy_process_group()
+        try:
+            if pg_ok:
+                dist.destroy_process_group()
+        except Exception:  # teardown after a failed side leg: the line is already out
+            pass
 
 
 if __name__ == "__main__":
