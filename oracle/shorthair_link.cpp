@@ -101,7 +101,11 @@ int main(int argc, char **argv) {
     server.peer = &client;
     client.peer = &server;
     server.lossy = true;
-    Settings ss, cs;
+    Settings ss, cs;  // the Tester's settings (Tester.cpp: Accept / Connect)
+    ss.min_fec_overhead = cs.min_fec_overhead = 0.2f;
+    ss.max_delay = cs.max_delay = 100;
+    ss.max_data_size = 1350;
+    cs.max_data_size = 1400;
     ss.interface_ptr = &server;
     cs.interface_ptr = &client;
     if (!server.codec.Initialize(ss) || !client.codec.Initialize(cs)) {
