@@ -115,6 +115,16 @@ def body(mode):
                 L.append(f"s_mov_b32 m0, {8 * j}")
             L += snippet(c, [])
         L.append("s_set_gpr_idx_off")
+    elif mode in ("call64r", "call128r"):  # as call72r with 64- / 128-byte snippet slots
+        stride = 64 if mode == "call64r" else 128
+        L.append("s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)")
+        for j in range(8):
+            if j:
+                L.append(f"s_set_gpr_idx_idx {8 * j}")
+            L += ["s_mul_i32 s49, s49, 0x41c64e6d", "s_add_u32 s49, s49, 12345",
+                  "s_lshr_b32 s50, s49, 24", f"s_mul_i32 s50, s50, {stride}",
+                  "s_add_u32 s42, s44, s50", "s_addc_u32 s43, s45, 0", "s_swappc_b64 s[40:41], s[42:43]"]
+        L.append("s_set_gpr_idx_off")
     elif mode == "call72r":  # idx mode, one table, coefficient varies per call (s49 = LCG state)
         L.append("s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)")
         for j in range(8):
@@ -185,6 +195,22 @@ def kernel(mode):
                     "v_mul_u32_u24 v21, 41, v21", "v_and_b32 v21, 255, v21", "v_mul_u32_u24 v21, 72, v21",
                     "v_add_u32 v20, s44, v21"]
         tables = ["s_branch jp_t72e" + mode] + table("jp_tab72" + mode, 3, ["s_setpc_b64 s[40:41]", "s_nop 0"]) + ["jp_t72e" + mode + ":"]
+    if mode in ("call64r", "call128r"):
+        lab = "jp_tab" + mode
+        pre = ["s_getpc_b64 s[44:45]", f"s_add_u32 s44, s44, {lab}@rel32@lo+4", f"s_addc_u32 s45, s45, {lab}@rel32@hi+12",
+               "s_mov_b32 s49, 1"]
+        t = ["s_branch " + lab + "_end", ".p2align 7", lab + ":"]
+        for c in range(256):
+            t.append(".p2align 6" if mode == "call64r" else ".p2align 7")
+            v = c
+            for bb in range(8):
+                if bb == 7 and mode == "call64r":  # 7 bitop3 + one VOP2 xor + return = 64 bytes
+                    t.append(f"v_xor_b32 v{ACC + bb}, v{T0 + (v & 15)}, v{ACC + bb}")
+                else:
+                    t.append(f"v_bitop3_b32 v{ACC + bb}, v{ACC + bb}, v{T0 + (v & 15)}, v{T1 + (v >> 4)} bitop3:0x96")
+                v = gmul2(v)
+            t.append("s_setpc_b64 s[40:41]")
+        tables = t + [lab + "_end:"]
     if mode == "call72r":
         pre = ["s_getpc_b64 s[44:45]", "s_add_u32 s44, s44, jp_tab72r@rel32@lo+4", "s_addc_u32 s45, s45, jp_tab72r@rel32@hi+12",
                "s_mov_b32 s49, 1"]
@@ -243,7 +269,7 @@ def kernel(mode):
 '''
 
 
-MODES = ["noidx", "idx0", "inline", "idxnop", "m0mov", "call1", "callidx0", "v2"]
+MODES = ["noidx", "call72r", "call64r", "call128r", "v2"]
 
 
 def main():
