@@ -46,6 +46,8 @@
 
 #include "geometry.hpp"
 
+#include <type_traits>
+
 namespace sh {
 namespace fixed {
 
@@ -128,6 +130,7 @@ __device__ __forceinline__ uint32_t col_off(int q, const Geometry &geo) {
 
 template <class S, bool DEC>
 struct Src {
+    static constexpr bool kStream = false;
     __amdgpu_buffer_rsrc_t rsrc;
     uint32_t dbase[S::DPW];   // chunk source offset, block 0 / array slot 0 (OOR past the batch)
     int dgl[S::DPW];          // decode: the chunk's group (position-table index)
@@ -231,6 +234,68 @@ struct Src {
 
 };
 
+// One-part shapes (P = 1): nothing is shared between the waves of a workgroup -- each column-wave
+// alone consumes its columns -- so the LDS ring is pure overhead there: its DMA, the round trip
+// through LDS and a workgroup barrier every step (the (28,4) ring holds only 4 slots of 16 KB).
+// StreamSrc keeps the generated schedule but loads each lane's 8 words of a step straight into
+// registers (8 coalesced buffer_load_dword: 64 consecutive columns of one sub-block per
+// instruction, any byte alignment), R steps ahead; the compiler's own vmcnt waits guard each use,
+// and no wave waits for another until the epilogue's row images.
+template <class S, bool DEC>
+struct StreamSrc {
+    static constexpr bool kStream = true;
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t lane_base;       // this lane's column in its group (OOR: past the batch)
+    int gl;                   // decode: the lane's group (position-table index)
+    uint32_t B, sub;
+    const uint8_t *pos;
+    mutable uint32_t buf[S::R][8];  // step x in buf[x % R] (compile-time indices after inlining)
+
+    __device__ __forceinline__ void init(const FixedArgs &a, const WGInfo &w, const uint8_t *, const uint8_t *lds_pos) {
+        const Geometry &geo = a.geo;
+        rsrc = wg_rsrc(a.in, a.in_bytes, a.in_gstride, w.g_first);
+        B = geo.B;
+        sub = geo.sub;
+        pos = lds_pos;
+        gl = w.gl;
+        lane_base = w.valid ? static_cast<uint32_t>(w.gl) * static_cast<uint32_t>(a.in_gstride) + col_off(w.q, geo) : OOR;
+    }
+    template <int T, int I>
+    __device__ __forceinline__ void wait() const {}
+    __device__ __forceinline__ static void release() {
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    struct Pre {
+        int p;
+    };
+    __device__ __forceinline__ Pre pre(int t) const {
+        Pre r;
+        r.p = DEC ? pos[gl * (S::KP + S::MP) + t] : 0;
+        return r;
+    }
+    __device__ __forceinline__ void issue(int x, const Pre &pr) const {
+        uint32_t o = lane_base, so = 0;
+        if (DEC)
+            o = (pr.p == 0xFF || lane_base == OOR) ? OOR : lane_base + static_cast<uint32_t>(pr.p) * B;
+        else
+            so = static_cast<uint32_t>(x) * B;
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+            buf[x % S::R][s] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, o == OOR ? OOR : o + s * sub, so, SH_LOAD_AUX);
+    }
+    __device__ __forceinline__ void read(int slot, uint32_t &d0, uint32_t &d1, uint32_t &d2, uint32_t &d3,
+                                         uint32_t &d4, uint32_t &d5, uint32_t &d6, uint32_t &d7) const {
+        d0 = buf[slot][0];
+        d1 = buf[slot][1];
+        d2 = buf[slot][2];
+        d3 = buf[slot][3];
+        d4 = buf[slot][4];
+        d5 = buf[slot][5];
+        d6 = buf[slot][6];
+        d7 = buf[slot][7];
+    }
+};
+
 // Output assembled per row across the part's CW column-waves, so every store instruction writes
 // 64 consecutive 16-byte pieces of the output in MEMORY order (about 1 KB contiguous): the
 // CW waves of a part write their words of row y into a shared LDS row image laid out like a ring
@@ -305,8 +370,8 @@ struct RowSink {
 // lanes) and returns this wave's part. The caller (the FIXED_KERNEL macro)
 // then calls the generated run_<name> directly, so everything inlines into one function: a
 // non-inlined body took `src` by reference through scratch and read the LDS ring with flat loads.
-template <class S, bool DEC>
-__device__ __forceinline__ int kernel_prologue(const FixedArgs &a, uint8_t *lds, Src<S, DEC> &src,
+template <class S, bool DEC, class SrcT>
+__device__ __forceinline__ int kernel_prologue(const FixedArgs &a, uint8_t *lds, SrcT &src,
                                                RowSink<S> &sink, long long col0, long long lo, long long hi) {
     WGInfo w;
     w.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -326,7 +391,7 @@ __device__ __forceinline__ int kernel_prologue(const FixedArgs &a, uint8_t *lds,
     w.gl = g - w.g_first;
     // The row images of the epilogue alias the start of the ring: they are used only after the
     // last step, behind Src::release()'s barrier, so the ring gets that LDS as extra slots.
-    uint8_t *lds_pos = lds + S::R * S::SLOT;
+    uint8_t *lds_pos = lds + (SrcT::kStream ? 2 * S::P * S::SLOT : S::R * S::SLOT);
     if (DEC) {
         const int ng = a.groups_per_wg;
         const int ghi = static_cast<int>(hi / nq);
@@ -364,12 +429,13 @@ __device__ __forceinline__ int xcd_tile(int b, int n) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
 
-template <class S, bool DEC>
+template <class S, bool DEC, bool STREAM = false>
 inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArgs)) {
     constexpr bool dec = DEC;
     a.groups_per_wg = (S::COLS - 1) / a.geo.nq + 2;
-    const size_t lds = static_cast<size_t>(S::R) * S::SLOT +  // ring (store scratch aliases it)
-                       (dec ? static_cast<size_t>(a.groups_per_wg) * (S::KP + S::MP) : 0);
+    // ring (the row images of the epilogue alias it); a streaming source needs only the images
+    constexpr size_t front = STREAM ? 2ull * S::P * S::SLOT : static_cast<size_t>(S::R) * S::SLOT;
+    const size_t lds = front + (dec ? static_cast<size_t>(a.groups_per_wg) * (S::KP + S::MP) : 0);
     const long long cols = static_cast<long long>(a.groups) * a.geo.nq;
     const unsigned blocks = static_cast<unsigned>((cols + S::COLS - 1) / S::COLS);  // one tile each
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(S::NT), lds, s, a);
@@ -382,13 +448,14 @@ inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArg
 // One kernel + launcher of a generated (k, m): MODE enc (DEC = false) or dec (DEC = true);
 // MINW = waves per SIMD the registers are allocated for. The host routes shapes with
 // nq % 4 != 0 (a 16-byte chunk could straddle two groups) or sub < 16 to the generic kernel.
-#define FIXED_KERNEL(NAME, K, M, P, CW, R, MINW, MODE, DEC, DMA)                                  \
+#define FIXED_KERNEL(NAME, K, M, P, CW, R, MINW, MODE, DEC, DMA, STREAM)                          \
     namespace sh {                                                                                \
     namespace fixed {                                                                             \
     __global__ __launch_bounds__(64 * CW * P, MINW) void kern_##NAME##_##MODE(FixedArgs a) {      \
         extern __shared__ __attribute__((aligned(16))) uint8_t lds[];                             \
         using S = Shape<K, M, P, CW, R, DMA>;                                                     \
-        Src<S, DEC> src;                                                                          \
+        using SrcT = typename std::conditional<STREAM, StreamSrc<S, DEC>, Src<S, DEC>>::type;     \
+        SrcT src;                                                                                 \
         RowSink<S> sink;                                                                          \
         const long long c0 = static_cast<long long>(xcd_tile(blockIdx.x, gridDim.x)) * S::COLS;  \
         const int part = kernel_prologue<S, DEC>(a, lds, src, sink, c0, 0,                       \
@@ -396,7 +463,7 @@ inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArg
         run_##NAME##_##MODE(part, src, sink);                                                     \
     }                                                                                             \
     hipError_t launch_##NAME##_##MODE(FixedArgs a, hipStream_t s) {                               \
-        return launch_shape<Shape<K, M, P, CW, R, DMA>, DEC>(a, s, kern_##NAME##_##MODE);         \
+        return launch_shape<Shape<K, M, P, CW, R, DMA>, DEC, STREAM>(a, s, kern_##NAME##_##MODE); \
     }                                                                                             \
     }                                                                                             \
     }

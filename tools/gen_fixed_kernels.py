@@ -255,7 +255,15 @@ def shape(k, m):
     minw = int(os.environ.get("SH_MIN_WAVES", minw_default or ("2" if rows > 12 else ("3" if rows > 8 else "4"))))
     # blocks per barrier: R >= 2*SYNC + 1 keeps >= 1 group of DMA in flight past the one waited for
     sync = int(os.environ.get("SH_SYNC", str(max(1, min(4, (R - 1) // 2 - 1)))))
+    if stream_mode(P):
+        R = int(os.environ.get("SH_STREAM_R", "6"))  # register buffers: steps loaded ahead
     return P, CW, R, minw, sync
+
+
+def stream_mode(P):
+    """One-part shapes may load each lane's words straight into registers (StreamSrc in
+    fixed_common.hpp) instead of through the LDS ring."""
+    return P == 1 and os.environ.get("SH_STREAM", "0") == "1"
 
 
 def gen_config(k, m):
@@ -333,7 +341,7 @@ def gen_config(k, m):
             f.write(f"// GENERATED by tools/gen_fixed_kernels.py -- do not edit. (k={k}, m={m}, {mode})\n"
                     f'#include "fixed_{name}.inc"\n'
                     f"FIXED_KERNEL({name}, {k}, {m}, {P}, {CW}, {R}, {minw}, {mode}, {dec}, "
-                    f"{'false' if 'nodma' in ABLATE else 'true'})\n")
+                    f"{'false' if 'nodma' in ABLATE else 'true'}, {'true' if stream_mode(P) else 'false'})\n")
         paths.append(path)
     return paths
 
