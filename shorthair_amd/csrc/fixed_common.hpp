@@ -316,7 +316,6 @@ struct RowSink {
     uint32_t wofs;            // this lane's word in a row image (tile column * 4)
     uint32_t B;
     uint8_t *img;             // this part's row image, even rows (odd rows: + P * SLOT)
-    static_assert(2 * S::P * S::SLOT <= S::R * S::SLOT, "row images must fit inside the ring");
 
     __device__ __forceinline__ void init(const FixedArgs &a, const WGInfo &w, int part, uint8_t *lds) {
         const Geometry &geo = a.geo;
@@ -435,6 +434,7 @@ inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArg
     a.groups_per_wg = (S::COLS - 1) / a.geo.nq + 2;
     // ring (the row images of the epilogue alias it); a streaming source needs only the images
     constexpr size_t front = STREAM ? 2ull * S::P * S::SLOT : static_cast<size_t>(S::R) * S::SLOT;
+    static_assert(STREAM || 2 * S::P <= S::R, "row images must fit inside the ring");
     const size_t lds = front + (dec ? static_cast<size_t>(a.groups_per_wg) * (S::KP + S::MP) : 0);
     const long long cols = static_cast<long long>(a.groups) * a.geo.nq;
     const unsigned blocks = static_cast<unsigned>((cols + S::COLS - 1) / S::COLS);  // one tile each

@@ -263,7 +263,8 @@ def shape(k, m):
 def stream_mode(P):
     """One-part shapes may load each lane's words straight into registers (StreamSrc in
     fixed_common.hpp) instead of through the LDS ring."""
-    return P == 1 and os.environ.get("SH_STREAM", "0") == "1"
+    mode = os.environ.get("SH_STREAM", "0")
+    return mode == "all" or (P == 1 and mode == "1")
 
 
 def gen_config(k, m):
