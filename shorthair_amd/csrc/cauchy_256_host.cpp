@@ -953,8 +953,35 @@ extern "C" int cauchy_256_sync(void *stream) {
 // =============================================================================================
 // Drop-in single-group ABI (cauchy_256.h). One group per call through pinned staging.
 // =============================================================================================
+// The reference's exported product/quotient tables (cauchy_256.cpp:346-347, built by GFC256Init
+// :349-386 on the first _cauchy_256_init): 256 x 256 bytes each, entry (y << 8) + x = x * y and
+// x / y in GF(256)/0x187, zero rows and columns for 0. Exported for symbol parity with
+// cauchy_256.o; the codec itself does not read them. Null until the first successful version check.
+extern "C" {
+__attribute__((visibility("default"))) uint8_t *GFC256_MUL_TABLE = nullptr;
+__attribute__((visibility("default"))) uint8_t *GFC256_DIV_TABLE = nullptr;
+}
+
+namespace {
+void export_field_tables() {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        static uint8_t tab[2][256 * 256];
+        const sh::GF256 &f = sh::gf();
+        for (int y = 0; y < 256; ++y)
+            for (int x = 0; x < 256; ++x) {
+                tab[0][(y << 8) + x] = f.mul(static_cast<uint8_t>(x), static_cast<uint8_t>(y));
+                tab[1][(y << 8) + x] = f.div(static_cast<uint8_t>(x), static_cast<uint8_t>(y));
+            }
+        GFC256_DIV_TABLE = tab[1];
+        GFC256_MUL_TABLE = tab[0];
+    });
+}
+}  // namespace
+
 extern "C" int _cauchy_256_init(int expected_version) {
     if (expected_version != CAUCHY_256_VERSION) return -1;  // reference cauchy_256.cpp:392-394
+    export_field_tables();
     Context &c = ctx();
     std::lock_guard<std::mutex> g(c.mu);
     return init_locked(c, c.device);

@@ -54,6 +54,18 @@ def test_version_mismatch_is_rejected_without_gpu():
     assert shorthair_amd.lib._cauchy_256_init(3) == -1
 
 
+def test_field_table_pointers_exported():
+    """cauchy_256.o's two data symbols (cauchy_256.cpp:346-347) are exported, null until a
+    successful _cauchy_256_init (filled on the GPU box: test_gpu_parity)."""
+    import shorthair_amd
+    out = subprocess.run(["nm", "-D", "--defined-only", shorthair_amd.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    data = {line.split()[-1] for line in out.splitlines() if line.split()[1] in ("B", "D")}
+    assert {"GFC256_MUL_TABLE", "GFC256_DIV_TABLE"} <= data
+    # no GPU here, so no _cauchy_256_init has succeeded in this process
+    assert ctypes.c_void_p.in_dll(shorthair_amd.lib, "GFC256_MUL_TABLE").value is None
+
+
 def test_headers_have_no_torch_or_cpp_types():
     for h in os.listdir(INCLUDE):
         text = re.sub(r"/\*.*?\*/", " ", open(os.path.join(INCLUDE, h)).read(), flags=re.S)

@@ -404,3 +404,25 @@ def test_c5_per_gpu_shard_131072_groups(sh):
         rc, nr = ora.decode(k, m, b, list(rows[g]), B)
         assert rc == 0 and nr == d_rows[g].cpu().numpy().tolist(), g
         assert np.array_equal(np.stack(b), blocks[g].cpu().numpy()), g
+
+
+def test_exported_field_tables_match_oracle(sh):
+    """GFC256_MUL_TABLE / GFC256_DIV_TABLE (cauchy_256.cpp:346-386): after init, entry (y << 8) + x
+    is x * y and x / y, the oracle's field (both full 64K tables)."""
+    lib = sh.lib
+    ora = po.oracle().lib
+    mul = np.ctypeslib.as_array(ctypes.cast(ctypes.c_void_p.in_dll(lib, "GFC256_MUL_TABLE").value,
+                                            ctypes.POINTER(ctypes.c_ubyte)), shape=(256, 256)).copy()
+    div = np.ctypeslib.as_array(ctypes.cast(ctypes.c_void_p.in_dll(lib, "GFC256_DIV_TABLE").value,
+                                            ctypes.POINTER(ctypes.c_ubyte)), shape=(256, 256)).copy()
+    exp_mul = np.array([[ora.ora_gf_mul(x, y) for x in range(256)] for y in range(256)], np.uint8)
+    exp_div = np.array([[ora.ora_gf_div(x, y) if y else 0 for x in range(256)] for y in range(256)], np.uint8)
+    assert np.array_equal(mul, exp_mul)
+    assert np.array_equal(div, exp_div)
+    assert mul[0x80, 2] == 0x87  # 2 * 0x80 reduced by the polynomial 0x187
+    ref = po.reference()  # the reference's own tables, when oracle/_ref was built
+    if ref is not None:
+        for name, ours in (("GFC256_MUL_TABLE", mul), ("GFC256_DIV_TABLE", div)):
+            p = ctypes.c_void_p.in_dll(ref.lib, name).value
+            theirs = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_ubyte)), shape=(256, 256))
+            assert np.array_equal(ours, theirs), name
