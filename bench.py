@@ -354,7 +354,7 @@ def packet_groups(args, k, m, B):
 # BASELINE.json config 2 (C2), config 4 (C4 sweep: k+m in {32,128,256} x B in {256,1400,64KiB},
 # m = (k+m)/8 as SURVEY §8d suggests) and the shapes catid/shorthair's Tester actually issues
 # (Shorthair.cpp:502-504 clamps m to 256-k).
-SWEEP = [("C2", 64, 16, 1400)] + [("C4", k, m, B) for (k, m) in ((28, 4), (112, 16), (224, 32))
+SWEEP = [("C2", 64, 16, 1400), ("C2 4096 groups", 64, 16, 1400, 4096)] + [("C4", k, m, B) for (k, m) in ((28, 4), (112, 16), (224, 32))
                                   for B in (256, 1400, 65536)] + \
         [("tester", 200, 56, 1352), ("tester", 190, 66, 1336), ("tester", 190, 66, 1344)] + \
         [("off-grid", 120, 136, 1400), ("off-grid", 150, 40, 1400), ("off-grid", 50, 10, 1000),
@@ -363,10 +363,11 @@ SWEEP = [("C2", 64, 16, 1400)] + [("C4", k, m, B) for (k, m) in ((28, 4), (112, 
 
 def sweep(args, sh, torch, s):
     """Per-shape device time of encode and decode (e = m worst case) with algorithmic GB/s and
-    fraction of the HBM peak, ~1.5 GB of input per op; plus C3 (random e in 1..32)."""
+    fraction of the HBM peak, ~1.5 GB of input per op unless the entry fixes its group count (C2 at
+    BASELINE.json's 4096 groups); plus C3 (random e in 1..32)."""
     out = []
-    for tag, k, m, B in SWEEP:
-        G = max(8, int(1.5e9 // (k * B)))
+    for tag, k, m, B, *fixed in SWEEP:
+        G = fixed[0] if fixed else max(8, int(1.5e9 // (k * B)))
         data = torch.empty((G, k, B), dtype=torch.uint8, device="cuda")
         rec = torch.empty((G, m, B), dtype=torch.uint8, device="cuda")
         sh.fill_synthetic(data, k, B, G, 0, 0x5E, s)
