@@ -152,64 +152,103 @@ def cpu_baseline(k, m, B, e_fixed, seconds, threads):
                 cpu=cpu_model(), modes=modes)
 
 
-def root_window_chunk(world, G, k, m, B, window_bytes=16e9):
-    """Groups per rank per chunk of the root-resident leg: the root holds one window of
-    world * chunk groups (inputs + recovery), never the whole batch (C5 is 280 GB of input)."""
-    per = world * (k + m) * B
-    return int(max(1, min(G, window_bytes // per)))
-
-
-def root_resident(args, sh, shd, dist, torch, rank, world, G, k, m, B, s, enc_in, enc_out):
-    """Groups stream through rank 0's GPU: per chunk, one RCCL scatter of world x chunk input
-    groups from the root's window over xGMI, encode on every GPU, one RCCL gather of the recovery
-    groups back into the root's window (north_star's root-resident flow), until every rank has
-    coded its whole shard. The root holds only the window, so the leg runs at C5 scale (1M groups:
-    280 GB of input, more than one GPU's HBM). Reported beside the main line, never as `value`."""
-    chunk = args.root_chunk or root_window_chunk(world, G, k, m, B)
+def root_resident(args, sh, shd, dist, torch, rank, world, G, k, m, B, s, enc_in, enc_out,
+                  dec_in, rows, dec_out, dec_rows, dec_cnt, es):
+    """Groups start and end on rank 0's GPU (north_star's root-resident flow), for
+    both ops, streamed through a window on the root (shd.RootStream: chunk j+1's RCCL scatter
+    and chunk j's RCCL gather overlap chunk j's kernels):
+      encode: scatter k*B data bytes per group, encode, gather m*B recovery bytes;
+      decode: scatter the k*B received blocks + the k-byte row array per group, decode_batch_out,
+              gather the e*B recovered blocks + their rows + the count.
+    The root holds one window per op (~16 GB), never the whole batch, so the leg runs at C5 scale
+    (1M groups: 280 GB of input, more than one GPU's HBM). The window's inputs are copies of the
+    root's own first chunk of groups; after the warm-up pass the root codes its whole window
+    itself and checks every rank's slot of the last chunk against it. Reported beside the main
+    line, never as `value`."""
     sizes = [shd.shard(args.total_groups, world, r)[1] for r in range(world)] if args.total_groups else [G] * world
-    nchunks = shd.chunk_count(sizes, chunk)
-    root_in = root_rec = None
-    if rank == 0:
-        root_in = torch.empty((world * chunk, k, B), dtype=torch.uint8, device="cuda")
-        root_rec = torch.empty((world * chunk, m, B), dtype=torch.uint8, device="cuda")
-        sh.fill_synthetic(root_in, k, B, world * chunk, 0, 0xBE, s)
-    partial = any(n % chunk for n in sizes)
-    st_in = torch.empty((chunk, k, B), dtype=torch.uint8, device="cuda") if partial else None
-    st_out = torch.empty((chunk, m, B), dtype=torch.uint8, device="cuda") if partial else None
-    torch.cuda.synchronize()
+    emax = min(k, m)
+    window = float(os.environ.get("SH_ROOT_WINDOW_BYTES", "16e9"))  # smaller: tests only
+    out = {}
 
-    def one_pass():
-        for j in range(nchunks):
-            n = shd.scatter_chunk(enc_in, j, chunk, root_in, st_in)
-            if n:
-                assert sh.encode_batch(k, m, B, n, enc_in[j * chunk:], enc_out[j * chunk:], s) == 0
-            shd.gather_chunk(enc_out, j, chunk, root_rec, st_out)
+    def leg(name, per_group, ins, outs, compute, make_win, check):
+        chunk = args.root_chunk or shd.root_chunk_size(sizes, per_group, window)
+        rs = shd.RootStream(sizes, chunk, ins, outs)
+        win_in = win_out = None
+        if rank == 0:
+            win_in = make_win(chunk)
+            win_out = [torch.zeros((world * chunk,) + tuple(t.shape[1:]), dtype=t.dtype, device="cuda") for t in outs]
+        torch.cuda.synchronize()
+        rs.run(compute, win_in, win_out)  # warm-up, and the pass the check reads
+        torch.cuda.synchronize()
+        ok = check(rs, chunk, win_in, win_out) if rank == 0 else None
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.root_steps):
+            rs.run(compute, win_in, win_out)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = shd.max_over_ranks(time.perf_counter() - t0, device="cuda")
+        del win_in, win_out
+        return {"chunk_groups_per_rank": chunk, "chunks": rs.nchunks,
+                "root_window_GB": round(world * chunk * per_group / 1e9, 2),
+                "ms_per_step": round(t / args.root_steps * 1e3, 4), "seconds": t, "roundtrip_ok": ok}
 
-    one_pass()  # warm-up (and the check below)
-    torch.cuda.synchronize()
-    ok = None
-    if rank == 0:
-        n0 = min(chunk, sizes[0])
-        lo = (nchunks - 1) * chunk  # the last chunk's window holds rank 0's groups [lo, lo + n)
-        n_last = max(0, min(chunk, sizes[0] - lo))
-        ok = bool(torch.equal(root_rec[:n_last], enc_out[lo:lo + n_last])) if n_last else bool(n0 == 0)
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.root_steps):
-        one_pass()
-    torch.cuda.synchronize()
-    dist.barrier()
-    t_root = shd.max_over_ranks(time.perf_counter() - t0, device="cuda")
+    # ---- encode ----
+    def enc_compute(lo, n):
+        assert sh.encode_batch(k, m, B, n, enc_in[lo:], enc_out[lo:], s) == 0
+
+    def enc_win(chunk):
+        return [enc_in[:chunk].repeat(world, 1, 1)]
+
+    def enc_check(rs, chunk, win_in, win_out):
+        exp = torch.empty_like(win_out[0])
+        assert sh.encode_batch(k, m, B, world * chunk, win_in[0], exp, s) == 0
+        torch.cuda.synchronize()
+        return all(bool(torch.equal(win_out[0][a:a + n], exp[a:a + n])) for _, a, n in rs.slots() if n)
+
+    r = leg("encode", (k + m) * B, [enc_in], [enc_out], enc_compute, enc_win, enc_check)
+    out["encode"] = dict(r, GiBps=round(sum(sizes) * (k + m) * B * args.root_steps / r.pop("seconds") / 2**30, 3),
+                         op="per chunk: RCCL scatter of data blocks, encode, RCCL gather of recovery blocks")
+
+    # ---- decode ----
+    def dec_compute(lo, n):
+        assert sh.decode_batch_out(k, m, B, n, dec_in[lo:], rows[lo:], dec_out[lo:], dec_rows[lo:],
+                                   dec_cnt[lo:], s) == 0
+
+    def dec_win(chunk):
+        return [dec_in[:chunk].repeat(world, 1, 1), rows[:chunk].repeat(world, 1)]
+
+    def dec_check(rs, chunk, win_in, win_out):
+        n_all = world * chunk
+        exp = [torch.empty_like(w) for w in win_out]
+        assert sh.decode_batch_out(k, m, B, n_all, win_in[0], win_in[1], *exp, s) == 0
+        torch.cuda.synchronize()
+        ok = True
+        for _, a, n in rs.slots():
+            if not n:
+                continue
+            cnt = exp[2][a:a + n]
+            ok &= bool(torch.equal(win_out[2][a:a + n], cnt))
+            ok &= bool(torch.equal(cnt.cpu(), torch.from_numpy(es[:chunk]).int().repeat(world)[a:a + n]))
+            mask = torch.arange(emax, device="cuda")[None, :] < cnt[:, None]
+            ok &= bool(torch.equal(win_out[1][a:a + n][mask], exp[1][a:a + n][mask]))
+            ok &= bool(torch.equal(win_out[0][a:a + n][mask], exp[0][a:a + n][mask]))
+        return ok
+
+    per_dec = k * B + k + emax * B + emax + 4
+    r = leg("decode", per_dec, [dec_in, rows], [dec_out, dec_rows, dec_cnt], dec_compute, dec_win, dec_check)
+    dec_bytes = int((k + es).sum()) * B  # this rank's algorithmic bytes; the totals below sum the ranks
+    dec_all = shd.sum_over_ranks(dec_bytes, device="cuda")
+    out["decode"] = dict(r, GiBps=round(dec_all * args.root_steps / r.pop("seconds") / 2**30, 3),
+                         op="per chunk: RCCL scatter of received blocks + rows, decode, RCCL gather of "
+                            "recovered blocks + rows + counts")
     if rank != 0:
         return None
-    total = sum(sizes)
-    return {"op": "per chunk: RCCL scatter from the root's window + encode + RCCL gather to the root",
-            "steps": args.root_steps, "chunk_groups_per_rank": chunk, "chunks": nchunks,
-            "root_window_GB": round(world * chunk * (k + m) * B / 1e9, 2),
-            "ms_per_step": round(t_root / args.root_steps * 1e3, 4),
-            "GiBps": round(total * (k + m) * B * args.root_steps / t_root / 2**30, 3),
-            "root_shard_roundtrip_ok": ok}
+    out["steps"] = args.root_steps
+    out["overlap"] = "chunk j+1 scatter and chunk j gather posted async around chunk j's kernels"
+    out["roundtrip_ok"] = bool(out["encode"]["roundtrip_ok"] and out["decode"]["roundtrip_ok"])
+    return out
 
 
 def host_path(args, sh, torch, k, m, B, s):
@@ -434,6 +473,34 @@ def _time_ops(args, sh, torch, s, k, m, B, G, data, rec, e_fixed, encode=True, i
     return r
 
 
+SIMDS = 1024           # 256 CUs x 4 SIMDs
+VALU_CYC = 2           # cycles per wave64 VALU instruction per SIMD at full rate (MI355X_MICROARCH.md)
+
+
+def valu_leg(sq, alg_bytes, launch_ms):
+    """The VALU leg of the roofline for the dominant kernel, from the SQ/GRBM pass of the
+    hash-matched PMC summary (per launch): lane-ops per algorithmic byte, VALU-busy fraction
+    (issue cycles per SIMD / elapsed cycles), the clock the chip held (GRBM_GUI_ACTIVE / 8 XCDs /
+    this run's launch time) and the VALU-issue floor at that clock, beside the HBM floor (algorithmic
+    bytes at 8 TB/s). `binding` names the larger floor."""
+    if not sq or not sq.get("SQ_INSTS_VALU") or not sq.get("GRBM_GUI_ACTIVE"):
+        return None
+    insts, cyc = sq["SQ_INSTS_VALU"], sq["GRBM_GUI_ACTIVE"] / 8
+    clock = cyc / (launch_ms * 1e-3)
+    floor_ms = insts * VALU_CYC / SIMDS / clock * 1e3
+    hbm_ms = alg_bytes / HBM_PEAK * 1e3
+    out = {"insts_per_launch": insts, "lane_ops_per_alg_byte": round(insts * 64 / alg_bytes, 3),
+           "busy_frac": round(insts * VALU_CYC / SIMDS / cyc, 4), "clock_GHz": round(clock / 1e9, 3),
+           "issue_floor_ms": round(floor_ms, 4), "hbm_floor_ms": round(hbm_ms, 4),
+           "binding": "valu" if floor_ms > hbm_ms else "hbm",
+           "note": "counters from the profiled (rocprofv3) launches of this build; clock uses this run's "
+                   "launch time, so it reads the clock under the counters' cycle count"}
+    if sq.get("SQ_WAVE_CYCLES"):
+        out["wait_frac"] = round(sq.get("SQ_WAIT_ANY", 0) / sq["SQ_WAVE_CYCLES"], 4)
+        out["issue_stall_frac"] = round(sq.get("SQ_WAIT_INST_ANY", 0) / sq["SQ_WAVE_CYCLES"], 4)
+    return out
+
+
 def pmc_traffic(sh, k, m, B, G, e):
     """Per-kernel HBM bytes per launch from the committed PMC summary (profiles/*/traffic*.json,
     written by tools/gpu_profile.sh: FETCH_SIZE and WRITE_SIZE in separate rocprofv3 passes,
@@ -572,7 +639,8 @@ def main():
     pg_ok = True
     if world > 1 and args.root_steps > 0:
         try:
-            root_res = root_resident(args, sh, shd, dist, torch, rank, world, G, k, m, B, s, enc_in, enc_out)
+            root_res = root_resident(args, sh, shd, dist, torch, rank, world, G, k, m, B, s, enc_in, enc_out,
+                                     dec_in, rows, dec_out, dec_rows, dec_cnt, es)
         except Exception as exc:  # never lose the main line over the side measurement
             root_res = {"error": f"{type(exc).__name__}: {exc}"}
             pg_ok = False
@@ -594,6 +662,7 @@ def main():
         # rows, like encode; stage B reads e residual rows and writes e recovered blocks
         alg = {"encode": kb, "decode_stageA": kb, "decode_stageB": 2 * e_all * B}
         traffic = None
+        valu = None
         pmc_line = None
         if pmc:
             pmc_line = {}
@@ -606,6 +675,7 @@ def main():
                                     "alg_bytes": alg[op], "traffic_over_alg": round(t["hbm_bytes"] / alg[op], 3)}
             dom_op = "encode" if dom[0].startswith("encode") else "decode_stageA"
             traffic = (find(names[dom_op]) or {}).get("hbm_bytes")
+            valu = valu_leg((find(names[dom_op]) or {}).get("sq"), kb, dom[1])
         threads = args.cpu_threads or host_cores()
         cpu = None if args.no_cpu else cpu_baseline(k, m, B, args.erasures, args.cpu_seconds, threads)
         line = {
@@ -633,12 +703,13 @@ def main():
                     "decode_ms": round(dec_ms, 4), "decode_GBps": round(dec_bw / 1e9, 1),
                     "decode_setup_ms": round(stages[0], 4), "decode_stageA_ms": round(stages[1], 4),
                     "decode_stageB_ms": round(stages[2], 4)},
-            "roofline": {"bound": "hbm", "kernel": dom[0], "achieved": round(kb / (dom[1] * 1e-3) / 1e9, 1),
+            "roofline": {"bound": (valu or {}).get("binding", "hbm"), "kernel": dom[0],
+                         "achieved": round(kb / (dom[1] * 1e-3) / 1e9, 1),
                          "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": round(kb / (dom[1] * 1e-3) / HBM_PEAK, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
                          "traffic_over_alg": round(traffic / kb, 3) if traffic else None,
-                         "alg_bytes_per_launch": kb, "launch_ms": round(dom[1], 4)},
+                         "alg_bytes_per_launch": kb, "launch_ms": round(dom[1], 4), "valu": valu},
             "op_roofline": {  # algorithmic bytes / measured time, as a fraction of 8 TB/s
                 "encode": round(enc_bytes / (enc_ms * 1e-3) / HBM_PEAK, 4),
                 "decode": round(dec_bytes / (dec_ms * 1e-3) / HBM_PEAK, 4),

@@ -77,8 +77,9 @@ int cauchy_256_erasure_pattern(unsigned long long g, int k, int m, unsigned long
 
 /* Which kernels code (k, m, block_bytes): 1 = compile-time-scheduled (generated for this (k, m)),
  * 2 = the runtime-coefficient tile kernels (any other (k, m) with block_bytes/8 >= 16),
- * 0 = the generic per-column kernels (shorter blocks), -1 = invalid parameters, -2 = no GPU
- * (the answer for shapes without generated kernels depends on where the code object loaded). */
+ * 0 = the generic per-column kernels (shorter blocks), -1 = invalid parameters. Host-only: never
+ * initialises the GPU. Before the library is initialised, 2 assumes the snippet table loaded
+ * inside one 4 GB page (checked at launch, generic kernels otherwise); afterwards it includes it. */
 int cauchy_256_batch_path(int k, int m, int block_bytes);
 
 /* The library's private stream (used by the single-group calls) and a synchronize helper for

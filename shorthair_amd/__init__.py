@@ -185,7 +185,8 @@ def has_fixed(k, m, block_bytes):
 
 def path(k, m, block_bytes):
     """Kernel family that codes (k, m, block_bytes): "fixed" (compile-time schedules), "tile"
-    (runtime-coefficient snippet tiles), "generic" (per-column kernels, B/8 < 16) or "invalid"."""
+    (runtime-coefficient snippet tiles), "generic" (per-column kernels, B/8 < 16) or "invalid".
+    Host-only: never initialises the GPU."""
     rc = lib.cauchy_256_batch_path(k, m, block_bytes)
     return {1: "fixed", 2: "tile", 0: "generic"}.get(rc, "invalid")
 

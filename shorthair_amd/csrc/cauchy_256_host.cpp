@@ -208,7 +208,10 @@ StreamState *stream_state(Context &c, hipStream_t stream) {
     if (!slot) {
         auto st = std::make_unique<StreamState>();
         if (hipMalloc(&st->d_errors, sizeof(int)) != hipSuccess) return nullptr;
-        if (hipMemset(st->d_errors, 0, sizeof(int)) != hipSuccess) return nullptr;
+        if (hipMemset(st->d_errors, 0, sizeof(int)) != hipSuccess) {
+            (void)hipFree(st->d_errors);
+            return nullptr;
+        }
         slot = std::move(st);
     }
     return slot.get();
@@ -897,10 +900,14 @@ extern "C" int cauchy_256_erasure_pattern(unsigned long long g, int k, int m, un
 extern "C" int cauchy_256_batch_path(int k, int m, int block_bytes) {
     if (k < 1 || m < 1 || k + m > 256 || block_bytes <= 0 || block_bytes % 8 != 0) return -1;
     if (sh::has_fixed(k, m, block_bytes) && !force_tile()) return 1;
+    // Host-only answer (a launcher may ask before it spawns rank processes, so this never
+    // initialises the GPU): the snippet table's one-4-GB-page condition needs the loaded code
+    // object and is checked at launch (generic kernels otherwise); once the library is
+    // initialised the answer includes it.
+    if (k < 2 || m < 2 || !sh::tile_ok(block_bytes) || std::getenv("SH_NO_TILE")) return 0;
     Context &c = ctx();
-    DeviceScope ds(c);
-    if (ds.rc) return ds.rc;
-    return tile_usable(c, k, m, block_bytes) ? 2 : 0;
+    std::lock_guard<std::mutex> g(c.mu);
+    return !c.ready || tile_usable(c, k, m, block_bytes) ? 2 : 0;
 }
 
 extern "C" void *cauchy_256_default_stream(void) {

@@ -452,36 +452,69 @@ __global__ __launch_bounds__(64 * W, 8) void decode_setup(DecodeSetupArgs a, int
         return;
     }
     fill_unused();  // the Gauss-Jordan below writes the (i < e, j < e) entries with put()
-    // m <= 6: Gauss-Jordan on [S | I] (e <= 5), one element per lane (lane = row * 2e + column),
-    // rows exchanged by cross-lane reads: a handful of dependent LDS trips per column instead of
-    // serial pivot scans and an LDS round trip per row.
-    const int w = 2 * e;
-    const int r = lane / w, c = lane - r * w;
-    const bool el = lane < e * w;
-    uint32_t v = 0;
-    if (el) v = c < e ? C(S.rrow[r], S.era[c]) : (c - e == r ? 1u : 0u);
+    // m <= 6: Gauss-Jordan on [S | I] (e <= m <= 6), element t = row * 2e + column held by lane
+    // t % 64 in half t / 64 (e * 2e <= 72, so two halves), rows exchanged by cross-lane reads: a
+    // handful of dependent LDS trips per column instead of serial pivot scans and an LDS round
+    // trip per row.
+    const int w = 2 * e, nel = e * w;
+    uint32_t v[2];
+    int r[2], c[2];
+    bool el[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int t = lane + 64 * h;
+        r[h] = t / w;
+        c[h] = t - r[h] * w;
+        el[h] = t < nel;
+        v[h] = !el[h] ? 0u : (c[h] < e ? C(S.rrow[r[h]], S.era[c[h]]) : (c[h] - e == r[h] ? 1u : 0u));
+    }
+    // value of element src (per lane; src < nel)
+    auto fetch = [&](int src) -> uint32_t {
+        const uint32_t lo = __shfl(v[0], src & 63), hi = __shfl(v[1], src & 63);
+        return src >= 64 ? hi : lo;
+    };
     auto gmul = [&](uint32_t x, uint32_t y) -> uint32_t {
         return (x && y) ? s_exp[s_log[x] + s_log[y]] : 0u;
     };
     for (int col = 0; col < e; ++col) {
-        const unsigned long long cand = __ballot(el && c == col && r >= col && v != 0);
-        if (cand == 0ull) {  // singular: impossible for an MDS submatrix
+        const unsigned long long c0 = __ballot(el[0] && c[0] == col && r[0] >= col && v[0] != 0);
+        const unsigned long long c1 = __ballot(el[1] && c[1] == col && r[1] >= col && v[1] != 0);
+        if ((c0 | c1) == 0ull) {  // singular: impossible for an MDS submatrix
             if (lane == 0) {
                 a.e_out[g] = -1;
                 if (a.errors) atomicAdd(a.errors, 1);
             }
             return;
         }
-        const int p = (__ffsll(static_cast<long long>(cand)) - 1) / w;  // wave-uniform pivot row
-        if (p != col) v = __shfl(v, r == col ? p * w + c : (r == p ? col * w + c : lane));
-        const uint32_t piv = __shfl(v, col * w + col);
+        // wave-uniform pivot row: the first candidate (elements are row-major)
+        const int p = c0 ? (__ffsll(static_cast<long long>(c0)) - 1) / w
+                         : (__ffsll(static_cast<long long>(c1)) - 1 + 64) / w;
+        if (p != col) {
+            uint32_t nv[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                nv[h] = fetch(r[h] == col ? p * w + c[h] : (r[h] == p ? col * w + c[h] : lane + 64 * h));
+            v[0] = nv[0];
+            v[1] = nv[1];
+        }
+        const uint32_t piv = fetch(col * w + col);
         const uint32_t pinv = s_exp[255 - s_log[piv]];
-        if (r == col) v = gmul(v, pinv);
-        const uint32_t f = __shfl(v, r * w + col);     // this row's entry in the pivot column
-        const uint32_t pc = __shfl(v, col * w + c);    // the pivot row's entry in this column
-        if (el && r != col) v ^= gmul(f, pc);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            if (r[h] == col) v[h] = gmul(v[h], pinv);
+        uint32_t f[2], pc[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            f[h] = fetch(el[h] ? r[h] * w + col : 0);    // this row's entry in the pivot column
+            pc[h] = fetch(el[h] ? col * w + c[h] : 0);   // the pivot row's entry in this column
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            if (el[h] && r[h] != col) v[h] ^= gmul(f[h], pc[h]);
     }
-    if (el && c >= e) put(r, c - e, v);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+        if (el[h] && c[h] >= e) put(r[h], c[h] - e, v[h]);
 }
 
 // In-place finish of decode: recovered erasure l (dense scratch) goes to the l-th recovery block

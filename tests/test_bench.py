@@ -77,7 +77,9 @@ def test_bench_two_ranks_on_one_gpu():
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["value"] > 0 and line["config"]["parallelism"] == "groups sharded x2"
-    assert line["root_resident"].get("root_shard_roundtrip_ok") is True
+    rr = line["root_resident"]
+    assert rr.get("roundtrip_ok") is True, rr
+    assert rr["encode"]["GiBps"] > 0 and rr["decode"]["GiBps"] > 0
 
 
 @pytest.mark.gpu
@@ -97,5 +99,25 @@ def test_bench_total_groups_chunked_root_two_ranks():
     assert line["n_gpus"] == 2 and line["scaling"] == "strong"
     assert line["config"]["total_groups"] == 301
     rr = line["root_resident"]
-    assert rr.get("root_shard_roundtrip_ok") is True, rr
-    assert rr["chunks"] == 3 and rr["chunk_groups_per_rank"] == 64
+    assert rr.get("roundtrip_ok") is True, rr
+    for op in ("encode", "decode"):
+        assert rr[op]["chunks"] == 3 and rr[op]["chunk_groups_per_rank"] == 64
+
+
+@pytest.mark.gpu
+def test_bench_uneven_shards_default_chunk():
+    """an odd --total-groups with the DEFAULT chunk (every rank derives it from the
+    largest shard) and a root window small enough for several chunks, the last one partial on one
+    rank only: both root-resident legs (encode, decode) round-trip."""
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ, SH_ROOT_WINDOW_BYTES=str(int(2 * 70 * (200 + 32) * 1400)))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                        "--steps", "1", "--warmup", "1", "--total-groups", "281",
+                        "--root-steps", "1", "--no-cpu", "--host-calls", "0", "--no-sweep"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rr = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])["root_resident"]
+    assert rr.get("roundtrip_ok") is True, rr
+    assert rr["encode"]["chunk_groups_per_rank"] == 70 and rr["encode"]["chunks"] == 3

@@ -89,58 +89,82 @@ def test_shard_partition(total, world):
     assert max(n for _, n in got) - min(n for _, n in got) <= 1
 
 
-def _chunk_worker(rank, world, port, q, total, chunk):
-    """Streamed root-resident pass (bench.py root_resident at C5 scale, scaled down): the root
-    holds one [world * chunk] window; every rank's shard (uneven: total % world != 0) arrives in
-    chunks and its "recovery" (shard ^ 0x5A, one row per group) goes back through the window."""
+def _stream_worker(rank, world, port, q, total, chunk, overlap):
+    """shd.RootStream at C5's shape, scaled down: the root holds one [world * chunk] window per
+    tensor; every rank's shard (uneven when total % world != 0) arrives in chunks -- two input
+    tensors, like decode's received blocks + row arrays -- and its outputs (three tensors, like
+    decode's recovered blocks + rows + counts) go back through the root's output windows. With
+    overlap, chunk j+1's scatter is in flight while chunk j computes."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from shorthair_amd import dist as d
         k, B = 3, 16
         sizes = [d.shard(total, world, r)[1] for r in range(world)]
+        if chunk is None:  # the default: every rank derives the same chunk from max(sizes)
+            chunk = d.root_chunk_size(sizes, k * B, window_bytes=world * 4 * k * B)
         g0, G = d.shard(total, world, rank)
-        n_chunks = d.chunk_count(sizes, chunk)
 
         def group_bytes(g):  # the root's content for global group g
             return (np.arange(k * B, dtype=np.int64) * 7 + g * 131).astype(np.uint8).reshape(k, B)
 
-        mine = torch.zeros((G, k, B), dtype=torch.uint8)
-        rec = torch.zeros((G, 1, B), dtype=torch.uint8)
-        st_in = torch.empty((chunk, k, B), dtype=torch.uint8)
-        st_out = torch.empty((chunk, 1, B), dtype=torch.uint8)
-        win_in = torch.empty((world * chunk, k, B), dtype=torch.uint8) if rank == 0 else None
-        win_out = torch.empty((world * chunk, 1, B), dtype=torch.uint8) if rank == 0 else None
+        blocks = torch.zeros((G, k, B), dtype=torch.uint8)
+        rows = torch.zeros((G, k), dtype=torch.uint8)
+        out = torch.zeros((G, 2, B), dtype=torch.uint8)
+        orow = torch.zeros((G, 2), dtype=torch.uint8)
+        cnt = torch.zeros(G, dtype=torch.int32)
+        rs = d.RootStream(sizes, chunk, [blocks, rows], [out, orow, cnt])
+        seen = []
+
+        def compute(lo, n):
+            seen.append((lo, n))
+            out[lo:lo + n] = blocks[lo:lo + n, :2] ^ 0x5A
+            orow[lo:lo + n] = rows[lo:lo + n, :2] + 1
+            cnt[lo:lo + n] = rows[lo:lo + n, 0].int() * 3
+
+        # the root's per-chunk windows (a real feeder refills double-buffered windows per chunk)
+        win_in = win_out = None
+        if rank == 0:
+            win_in, win_out = {}, {}
+            for j in range(rs.nchunks):
+                win_in[j] = [torch.zeros((world * chunk, k, B), dtype=torch.uint8),
+                             torch.zeros((world * chunk, k), dtype=torch.uint8)]
+                win_out[j] = [torch.zeros((world * chunk, 2, B), dtype=torch.uint8),
+                              torch.zeros((world * chunk, 2), dtype=torch.uint8),
+                              torch.zeros(world * chunk, dtype=torch.int32)]
+                for r in range(world):
+                    rg0, rn = d.shard(total, world, r)
+                    for i in range(max(0, min(chunk, rn - j * chunk))):
+                        g = rg0 + j * chunk + i
+                        win_in[j][0][r * chunk + i] = torch.from_numpy(group_bytes(g))
+                        win_in[j][1][r * chunk + i] = torch.tensor([g % 256, 1, 2], dtype=torch.uint8)
+        rs.run(compute, win_in and win_in.__getitem__, win_out and win_out.__getitem__, overlap=overlap)
         back_ok = True
-        for j in range(n_chunks):
-            if rank == 0:  # the root refills its window with chunk j of every rank's shard
-                win_in.zero_()
-                for r in range(world):
-                    rg0, rn = d.shard(total, world, r)
-                    for i in range(max(0, min(chunk, rn - j * chunk))):
-                        win_in[r * chunk + i] = torch.from_numpy(group_bytes(rg0 + j * chunk + i))
-            n = d.scatter_chunk(mine, j, chunk, win_in, st_in)
-            lo = j * chunk
-            rec[lo:lo + n] = mine[lo:lo + n, :1] ^ 0x5A
-            d.gather_chunk(rec, j, chunk, win_out, st_out)
-            if rank == 0:
-                for r in range(world):
-                    rg0, rn = d.shard(total, world, r)
-                    for i in range(max(0, min(chunk, rn - j * chunk))):
-                        want = group_bytes(rg0 + j * chunk + i)[:1] ^ 0x5A
-                        back_ok &= bool(np.array_equal(win_out[r * chunk + i].numpy(), want))
-        ok = all(np.array_equal(mine[i].numpy(), group_bytes(g0 + i)) for i in range(G))
-        q.put((rank, {"ok": ok, "back_ok": back_ok, "chunks": n_chunks, "G": G}))
+        if rank == 0:
+            for j in range(rs.nchunks):
+                for r, a, n in rs.slots(j):
+                    rg0 = d.shard(total, world, r)[0]
+                    for i in range(n):
+                        g = rg0 + j * chunk + i
+                        back_ok &= bool(np.array_equal(win_out[j][0][a + i].numpy(), group_bytes(g)[:2] ^ 0x5A))
+                        back_ok &= win_out[j][1][a + i].tolist() == [(g % 256) + 1, 2]
+                        back_ok &= int(win_out[j][2][a + i]) == (g % 256) * 3
+        ok = all(np.array_equal(blocks[i].numpy(), group_bytes(g0 + i)) for i in range(G))
+        ok &= sorted(seen) == [(lo, min(chunk, G - lo)) for lo in range(0, G, chunk)]
+        q.put((rank, {"ok": ok, "back_ok": back_ok, "chunks": rs.nchunks, "G": G, "chunk": chunk}))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,total,chunk", [(2, 11, 4), (3, 10, 3), (3, 9, 5)])
-def test_chunked_root_scatter_gather(world, total, chunk):
+@pytest.mark.parametrize("world,total,chunk,overlap", [(2, 11, 4, True), (3, 10, 3, True), (3, 9, 5, True),
+                                                       (2, 11, 4, False), (3, 13, None, True),
+                                                       (2, 3, 1, True)])
+def test_root_stream(world, total, chunk, overlap):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_chunk_worker, args=(r, world, port, q, total, chunk)) for r in range(world)]
+    procs = [ctx.Process(target=_stream_worker, args=(r, world, port, q, total, chunk, overlap))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(world))
@@ -148,23 +172,22 @@ def test_chunked_root_scatter_gather(world, total, chunk):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert sum(res[r]["G"] for r in range(world)) == total
+    assert len({res[r]["chunk"] for r in range(world)}) == 1  # every rank agrees on the chunk
     for r in range(world):
         assert res[r]["ok"], r
-        assert res[r]["chunks"] == -(-max(res[x]["G"] for x in range(world)) // chunk)
+        assert res[r]["chunks"] == -(-max(res[x]["G"] for x in range(world)) // res[r]["chunk"])
     assert res[0]["back_ok"]
 
 
 def test_c5_total_groups_and_root_window():
     """bench.py --gpus 8 --total-groups 1048576: 131,072 groups per rank; the root-resident leg's
     window at (200, 32, 1400) stays within ~16 GB of the root's HBM (the whole batch is 325 GB)."""
-    import importlib.util
     from shorthair_amd import dist as d
-    spec = importlib.util.spec_from_file_location("bench", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
-    bench = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(bench)
     sizes = [d.shard(1 << 20, 8, r)[1] for r in range(8)]
     assert sizes == [131072] * 8
-    chunk = bench.root_window_chunk(8, 131072, 200, 32, 1400)
+    chunk = d.root_chunk_size(sizes, (200 + 32) * 1400)
     assert 8 * chunk * (200 + 32) * 1400 <= 16e9 and chunk >= 4096
     assert d.chunk_count(sizes, chunk) * chunk >= 131072
-    assert bench.root_window_chunk(2, 100, 200, 32, 1400) == 100  # small batches: one chunk
+    assert d.root_chunk_size([100, 100], (200 + 32) * 1400) == 100  # small batches: one chunk
+    # uneven shards: the chunk follows the largest shard on every rank (ADVICE r3)
+    assert d.root_chunk_size([51, 50], 10, window_bytes=1e9) == 51

@@ -177,6 +177,10 @@ def _decode_inputs(k, m, B, G, cfg, e_fixed):
                                              (64, 16, 1400, 1024, 0), (28, 4, 256, 700, 0),
                                              (112, 16, 65536, 6, 0), (128, 128, 8, 64, 0),
                                              (30, 9, 48, 500, 9),
+                                             # e = m on the searched tables (two Gauss-Jordan
+                                             # elements per lane at e = 6)
+                                             (20, 6, 1400, 999, 6), (12, 5, 64, 300, 5),
+                                             (40, 6, 256, 513, 0),
                                              # small blocks on the compile-time path (stageb_small,
                                              # nq = 4 / 8 / 12 / 16 word columns, shifted chunks)
                                              (28, 4, 128, 3001, 0), (224, 32, 256, 601, 0),

@@ -25,6 +25,8 @@ import os
 import sys
 
 ROOT = os.path.normpath(os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+if os.path.dirname(os.path.abspath(__file__)) not in sys.path:  # tools/xor_sched.py
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 OUTDIR = os.path.join(ROOT, "shorthair_amd", "csrc", "gen")
 
 # (k, m): BASELINE.json configs -- headline (200,32), C2 (64,16), C4 sweep (28,4),(112,16),(224,32)
@@ -134,15 +136,19 @@ class Body:
         return name
 
     def emit(self, R, S, steps, KP):
-        """Software-pipelined steps (see fixed_common.hpp): step i waits for slot i+1, reads it
-        into the other register set, refills freed slots up to step i+R-1, and computes step i
-        from the registers read one iteration earlier. Sets alternate: dA (even i), dB.
-        steps: ("c", x) = input column x (position-table entry x), ("r", y) = decode only: the
-        received recovery block of generator row y (entry KP + y), added to row y's residual."""
+        """Software-pipelined units (see fixed_common.hpp). A unit is JOINT consecutive input
+        steps (a pair by default; recovery-row steps are single units) computed as one XOR
+        program (tools/xor_sched.py); while unit u computes, the words of unit u+1 are read from
+        the ring into the other register bank (dA / dB, 8 words per step). Before reading a unit
+        whose steps are not known to have landed, a wave waits (counted vmcnt) for the DMAs of the
+        next S steps and joins the workgroup barrier; every wave is then past the units before u,
+        so the ring slots of their steps are free and are refilled (up to R steps ahead) right
+        there. steps: ("c", x) = input column x (position-table entry x), ("r", y) = decode only:
+        the received recovery block of generator row y (entry KP + y), added to row y's residual."""
         L = self.lines
-        nr = self.y1 - self.y0
         n = len(steps)
         dma = "nodma" not in ABLATE
+        J = unit_steps(R)
 
         def tidx(st):
             return st[1] if st[0] == "c" else KP + st[1]
@@ -150,79 +156,220 @@ class Body:
         def uses(st):
             return st[0] == "c" or self.y0 <= st[1] < self.y1
 
-        L.append("    uint32_t dA0, dA1, dA2, dA3, dA4, dA5, dA6, dA7;")
-        L.append("    uint32_t dB0, dB1, dB2, dB3, dB4, dB5, dB6, dB7;")
+        units, i = [], 0
+        while i < n:
+            if J == 2 and i + 1 < n and steps[i][0] == "c" and steps[i + 1][0] == "c":
+                units.append([i, i + 1])
+                i += 2
+            else:
+                units.append([i])
+                i += 1
+        for bank in ("dA", "dB"):
+            L.append("    uint32_t " + ", ".join(f"{bank}{a}" for a in range(8 * J)) + ";")
+
+        def read_unit(u, bank):
+            for j, t in enumerate(units[u]):
+                if uses(steps[t]):
+                    L.append(f"    src.read({t % R}, " + ", ".join(f"{bank}{8 * j + a}" for a in range(8)) + ");")
+
         nxt_issue = min(n, R - 1)  # steps 0..nxt_issue-1 issued (in order)
         if dma:
             for t in range(nxt_issue):
                 L.append(f"    src.issue({t}, src.pre({tidx(steps[t])}));")
-        L.append(f"    src.template wait<{min(n, S) - 1}, {nxt_issue}>();")
-        if uses(steps[0]):
-            L.append("    src.read(0, " + ", ".join(f"dA{a}" for a in range(8)) + ");")
+        need = units[1][-1] if len(units) > 1 else units[0][-1]
+        landed = min(n - 1, max(need, S - 1), nxt_issue - 1)
+        assert need <= landed
+        L.append(f"    src.template wait<{landed}, {nxt_issue}>();")
+        read_unit(0, "dA")
         if nxt_issue < n:
             L.append(f"    typename Src::Pre pre = src.pre({tidx(steps[nxt_issue])});")
-        for i, st in enumerate(steps):
-            cur, nxt = ("dA", "dB") if i % 2 == 0 else ("dB", "dA")
-            L.append(f"    // ---- step {i}: " + (f"input block {st[1]}" if st[0] == "c" else f"recovery row {st[1]}"))
-            # Pin the step structure: without this hipcc hoists work across steps.
+        for u, unit in enumerate(units):
+            cur, nxt = ("dA", "dB") if u % 2 == 0 else ("dB", "dA")
+            L.append("    // ---- " + ", ".join(f"step {t}: " + (f"input block {steps[t][1]}" if steps[t][0] == "c"
+                                                                  else f"recovery row {steps[t][1]}") for t in unit))
+            # Pin the unit structure: without this hipcc hoists work across units.
             L.append("    __builtin_amdgcn_sched_barrier(0);")
-            if i + 1 < n:
-                if (i + 1) % S == 0:
+            if u + 1 < len(units):
+                nu = units[u + 1]
+                if nu[-1] > landed:
                     # group boundary: the next S steps must have landed (counted vmcnt) and every
-                    # wave must be past step i-1 (barrier), which frees the slots of steps <= i-1
+                    # wave must be past the units before this one (barrier), which frees their slots
+                    landed = min(n - 1, nu[-1] + S - 1, nxt_issue - 1)
+                    assert nu[-1] <= landed, "ring too small for the unit size"
                     if "nobar" not in ABLATE:
-                        L.append(f"    src.template wait<{min(n - 1, i + S)}, {nxt_issue}>();")
-                    while nxt_issue < n and nxt_issue - R <= i - 1:
+                        L.append(f"    src.template wait<{landed}, {nxt_issue}>();")
+                    while nxt_issue < n and nxt_issue - R <= unit[0] - 1:
                         if dma:
                             L.append(f"    src.issue({nxt_issue}, pre);")
                         nxt_issue += 1
                         if nxt_issue < n:
                             L.append(f"    pre = src.pre({tidx(steps[nxt_issue])});")
-                if uses(steps[i + 1]):
-                    L.append(f"    src.read({(i + 1) % R}, " + ", ".join(f"{nxt}{a}" for a in range(8)) + ");")
-                    if READ_PIN:
-                        # keep the next block's ds_reads at the top of the step: left free, the
-                        # scheduler sinks them to ~25 VALU before their use (LDS latency exposed)
-                        L.append("    __builtin_amdgcn_sched_barrier(0);")
-            if st[0] == "r":
-                if uses(st):  # residual row y += the received recovery block R_y (zeros if absent)
+                read_unit(u + 1, nxt)
+                if READ_PIN:
+                    # keep the next unit's ds_reads at the top of the unit: left free, the
+                    # scheduler sinks them to ~25 VALU before their use (LDS latency exposed)
+                    L.append("    __builtin_amdgcn_sched_barrier(0);")
+            cols = [t for t in unit if steps[t][0] == "c"]
+            L.append("    {")
+            if "novalu" in ABLATE:  # keep the loaded words alive, do no XOR work
+                L.append("    asm volatile(\"\" :: " + ", ".join(f'"v"({cur}{a})' for a in range(8 * len(cols))) + ");")
+            elif cols and JOINT == 0:
+                self.window_step(steps[cols[0]][1], cur)
+            elif cols:
+                self.slp_unit([steps[t][1] for t in cols], cur)
+            for j, t in enumerate(unit):
+                st = steps[t]
+                if st[0] == "r" and uses(st):  # residual row y += the received recovery block R_y
                     yi = st[1] - self.y0
                     for b in range(8):
-                        L.append(f"    XV(acc[{yi}][{b}], {cur}{b});")
-                    L.append(f"    PIN8(acc[{yi}]);")
-                continue
-            x = st[1]
-            L.append("    {")
-            have = set()
-            # Updates ordered by the high-half table entry: each T1 entry is built right before
-            # the updates that use it and dies after them (fewer live table registers).
-            ups = []
-            for yi in range(nr):
-                v = self.rows[self.y0 + yi][x]
-                for b in range(8):
-                    ups.append((v >> 4, v & 15, yi, b))
-                    v = gmul(v, 2)
-            ups.sort(key=lambda u: (u[0], u[1]))
-            if "novalu" in ABLATE:  # keep the loaded words alive, do no XOR work
-                L.append("    asm volatile(\"\" :: " + ", ".join(f'"v"({cur}{a})' for a in range(8)) + ");")
-                ups = []
-            for hi, lo, yi, b in ups:
-                acc = f"acc[{yi}][{b}]"
-                if lo and hi:
-                    ta = self.table_expr(0, lo, have, cur)
-                    tb = self.table_expr(1, hi, have, cur)
-                    L.append(f"    {acc} = X3({acc}, {ta}, {tb});")
-                elif lo:
-                    L.append(f"    XV({acc}, {self.table_expr(0, lo, have, cur)});")
-                else:
-                    L.append(f"    XV({acc}, {self.table_expr(1, hi, have, cur)});")
-            # Tie every accumulator to this step (an empty volatile asm is a chained side effect):
+                        L.append(f"    XV(acc[{yi}][{b}], {cur}{8 * j + b});")
+            # Tie every accumulator to this unit (an empty volatile asm is a chained side effect):
             # otherwise the DAG scheduler floats the pure bitop3 nodes of a ~30K-node basic block
             # away from their loads and keeps every loaded word live.
-            for yi in range(nr):
+            for yi in range(self.y1 - self.y0):
                 L.append(f"    PIN8(acc[{yi}]);")
             L.append("    }")
         return "\n".join(L)
+
+    def window_step(self, x, cur):
+        """One input block with the reference's 4-bit window tables (SH_JOINT=0, A/B only):
+        22 table XORs + one bitop3 per output row."""
+        L = self.lines
+        have = set()
+        # Updates ordered by the high-half table entry: each T1 entry is built right before
+        # the updates that use it and dies after them (fewer live table registers).
+        ups = []
+        for yi in range(self.y1 - self.y0):
+            v = self.rows[self.y0 + yi][x]
+            for b in range(8):
+                ups.append((v >> 4, v & 15, yi, b))
+                v = gmul(v, 2)
+        ups.sort(key=lambda u: (u[0], u[1]))
+        for hi, lo, yi, b in ups:
+            acc = f"acc[{yi}][{b}]"
+            if lo and hi:
+                ta = self.table_expr(0, lo, have, cur)
+                tb = self.table_expr(1, hi, have, cur)
+                L.append(f"    {acc} = X3({acc}, {ta}, {tb});")
+            elif lo:
+                L.append(f"    XV({acc}, {self.table_expr(0, lo, have, cur)});")
+            elif hi:
+                L.append(f"    XV({acc}, {self.table_expr(1, hi, have, cur)});")
+
+    def slp_unit(self, xs, cur):
+        """The unit's input blocks xs (1 or 2) as one XOR program: word bit 8j + a is input
+        sub-block a of block xs[j] (register {cur}{8j + a}); intermediates are defined right
+        before their first use, unused ones never."""
+        L = self.lines
+        nbits = 8 * len(xs)
+        tg = []
+        for yi in range(self.y1 - self.y0):
+            per = [row_bytes(self.rows[self.y0 + yi][x]) for x in xs]
+            for b in range(8):
+                tg.append(sum(per[j][b] << (8 * j) for j in range(len(xs))))
+        inters, reps = sched(tg, nbits)
+        order = {w: i for i, (w, _) in enumerate(inters)}
+        ops_of = dict(inters)
+        names = {}
+
+        def name(w):
+            if w & (w - 1) == 0:
+                return f"{cur}{w.bit_length() - 1}"
+            if w not in names:
+                ops = [name(o) for o in ops_of[w]]
+                names[w] = f"t{len(names)}"
+                expr = f"{ops[0]} ^ {ops[1]}" if len(ops) == 2 else f"X3({ops[0]}, {ops[1]}, {ops[2]})"
+                L.append(f"    const uint32_t {names[w]} = {expr};")
+            return names[w]
+
+        ups = [(yi, b, reps[t]) for (yi, b), t in zip(((yi, b) for yi in range(self.y1 - self.y0) for b in range(8)), tg) if t]
+        ups.sort(key=lambda u: max(order.get(w, -1) for w in u[2]))
+        for yi, b, rep in ups:
+            acc = f"acc[{yi}][{b}]"
+            ws = [name(w) for w in rep]
+            for q in range(0, len(ws) - 1, 2):
+                L.append(f"    {acc} = X3({acc}, {ws[q]}, {ws[q + 1]});")
+            if len(ws) % 2:
+                L.append(f"    XV({acc}, {ws[-1]});")
+
+
+# XOR programs per unit (tools/xor_sched.py), cached on disk by their exact targets: the greedy
+# search costs ~0.1 s per 16-bit unit, ~2,600 units over CONFIGS.
+JOINT = int(os.environ.get("SH_JOINT", "2"))  # steps per XOR program; 0 = the reference's window tables
+_SCHED = {}
+_CACHE = os.path.join(ROOT, "shorthair_amd", "csrc", "gen_cache", "xor_sched.json")
+
+
+def unit_steps(R):
+    """Steps per XOR program for a ring of R slots: pairs need the two slots of the unit being
+    prefetched plus DMA in flight beyond the waited group (R >= 8); the (28,4) ring has 4."""
+    return 2 if JOINT == 2 and R >= 8 else 1
+
+
+def _sched_key(tg, nbits):
+    return f"{nbits}:" + ",".join(f"{t:x}" for t in tg)
+
+
+def _sched_compute(key):
+    import xor_sched
+    nbits, body = key.split(":")
+    tg = [int(t, 16) for t in body.split(",")]
+    inters, reps, _ = (xor_sched.schedule_joint(tg, int(nbits)) if int(nbits) > 8 else xor_sched.schedule(tg))
+    return key, ([[int(w), [int(o) for o in ops]] for w, ops in inters], {str(t): list(r) for t, r in reps.items()})
+
+
+def sched(tg, nbits):
+    key = _sched_key(tg, nbits)
+    if key not in _SCHED:
+        _SCHED[key] = _sched_compute(key)[1]
+    inters, reps = _SCHED[key]
+    return [(w, tuple(ops)) for w, ops in inters], {int(t): tuple(r) for t, r in reps.items()}
+
+
+def load_sched_cache():
+    import json
+    try:
+        _SCHED.update(json.load(open(_CACHE)))
+    except (OSError, ValueError):
+        pass
+
+
+def save_sched_cache():
+    import json
+    os.makedirs(os.path.dirname(_CACHE), exist_ok=True)
+    with open(_CACHE + ".tmp", "w") as f:
+        json.dump(_SCHED, f)
+    os.replace(_CACHE + ".tmp", _CACHE)
+
+
+def prefetch_schedules(cfgs):
+    """Compute every unit's XOR program of `cfgs` that the cache lacks, on all host cores."""
+    if JOINT == 0:
+        return
+    keys = set()
+    for k, m in cfgs:
+        rows = generator(k, m)
+        P, _, R = shape(k, m)[:3]
+        J = unit_steps(R)
+        base, extra = divmod(m, P)
+        y0 = 0
+        for p in range(P):
+            y1 = y0 + base + (1 if p < extra else 0)
+            units = [list(range(x, min(k, x + J))) for x in range(0, k, J)]
+            for xs in units:
+                tg = []
+                for y in range(y0, y1):
+                    per = [row_bytes(rows[y][x]) for x in xs]
+                    tg += [sum(per[j][b] << (8 * j) for j in range(len(xs))) for b in range(8)]
+                keys.add(_sched_key(tg, 8 * len(xs)))
+            y0 = y1
+    todo = sorted(k for k in keys if k not in _SCHED)
+    if todo:
+        import multiprocessing as mp
+        with mp.get_context("fork").Pool(max(1, min(16, os.cpu_count() or 1))) as pool:
+            for key, val in pool.imap_unordered(_sched_compute, todo, chunksize=8):
+                _SCHED[key] = val
+        save_sched_cache()
 
 
 def shape(k, m):
@@ -541,6 +688,8 @@ def main(argv=()):
     cfgs = CONFIGS
     if argv:
         cfgs = [tuple(map(int, a.split(","))) for a in argv]
+    load_sched_cache()
+    prefetch_schedules(cfgs)
     paths = [p for (k, m) in cfgs for p in gen_config(k, m)]
     gen_snippets()
     gen_colsnips()

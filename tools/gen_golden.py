@@ -112,6 +112,10 @@ def main():
     dec_case("dec_k128_m128_e100_8", 43, 128, 128, 8, 100, order="shuffled")
     dec_case("dec_k3_m253_e3_8", 44, 3, 253, 8, 3)
     dec_case("dec_bad_km", 45, 200, 60, 16, 4, note="k+m>256: rc=-1 (:1271)")
+    # e = m at the searched tables (m <= 6): every recovery row replaces an erasure
+    dec_case("dec_m6_e6", 46, 20, 6, 40, 6, order="shuffled", note="m=6, e=6: 6x6 submatrix")
+    dec_case("dec_m6_e6_1400", 47, 30, 6, 1400, 6, note="m=6, e=6 at B=1400")
+    dec_case("dec_m5_e5", 48, 12, 5, 64, 5, order="reversed", note="m=5, e=5")
 
     # ---- config 1: the call shapes the reference's loopback Tester issues (SURVEY.md §3.4:
     # k=200/m=56/B=1352, k=190/m=66/B in {1336,1344}, decodes with 12-28 erasures). Tester.cpp

@@ -24,11 +24,11 @@ pmc() {  # pmc NAME COUNTERS...
 }
 pmc fetch FETCH_SIZE || exit 1
 pmc write WRITE_SIZE || exit 1
-python3 tools/traffic_json.py "$OUT" > "$OUT/traffic.json" || exit 1
-# bench.py reads profiles/*/traffic*.json (matched by the library hash): the run below sees it
-PROFDIR=${PROFDIR:-profiles/r03}; mkdir -p $PROFDIR && cp "$OUT/traffic.json" "$PROFDIR/traffic_$TAG.json"
 pmc sq GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_SALU || exit 1
 python3 tools/pmc_summary.py "$OUT/sq" > "$OUT/sq.txt"
+python3 tools/traffic_json.py "$OUT" > "$OUT/traffic.json" || exit 1
+# bench.py reads profiles/*/traffic*.json (matched by the library hash): the run below sees it
+PROFDIR=${PROFDIR:-profiles/r04}; mkdir -p $PROFDIR && cp "$OUT/traffic.json" "$PROFDIR/traffic_$TAG.json"
 if [ -n "${IFETCH:-}" ]; then  # e.g. IFETCH="SQC_ICACHE_REQ SQC_ICACHE_MISSES" (names from --list-avail)
   pmc ifetch $IFETCH || exit 1
   python3 tools/pmc_summary.py "$OUT/ifetch" > "$OUT/ifetch.txt"
