@@ -37,6 +37,7 @@ if os.environ.get("SH_CONFIGS"):  # experiments: e.g. SH_CONFIGS="200,32;64,16"
     CONFIGS = [tuple(map(int, c.split(","))) for c in os.environ["SH_CONFIGS"].split(";")]
 ROWS_PER_PART = int(os.environ.get("SH_ROWS_PER_PART", "8"))
 READ_PIN = os.environ.get("SH_READ_PIN", "0") == "1"
+READ_LATE = os.environ.get("SH_READ_LATE", "1") == "1"
 # Measurement-only ablations for A/B libraries built by tools/build_variant.sh (never the product
 # default, results are wrong), comma-separated: "nodma" = no input DMA (compute on whatever the
 # ring holds), "novalu" = DMA, ring reads, barriers and stores but no XOR work, "nobar" = no
@@ -110,8 +111,9 @@ def row_bytes(c):
 class Body:
     """Straight-line code for one part (rows y0..y1-1) over all k inputs."""
 
-    def __init__(self, k, rows, y0, y1):
+    def __init__(self, k, rows, y0, y1, rows_max=None):
         self.k, self.rows, self.y0, self.y1 = k, rows, y0, y1
+        self.rows_max = rows_max or (y1 - y0)  # the largest part of the kernel (one unit size for all)
         self.lines = []
 
     def table_expr(self, h, v, have, d):
@@ -148,7 +150,7 @@ class Body:
         L = self.lines
         n = len(steps)
         dma = "nodma" not in ABLATE
-        J = unit_steps(R)
+        J = unit_steps(R, self.rows_max)
 
         def tidx(st):
             return st[1] if st[0] == "c" else KP + st[1]
@@ -204,7 +206,8 @@ class Body:
                         nxt_issue += 1
                         if nxt_issue < n:
                             L.append(f"    pre = src.pre({tidx(steps[nxt_issue])});")
-                read_unit(u + 1, nxt)
+                if not READ_LATE:
+                    read_unit(u + 1, nxt)
                 if READ_PIN:
                     # keep the next unit's ds_reads at the top of the unit: left free, the
                     # scheduler sinks them to ~25 VALU before their use (LDS latency exposed)
@@ -229,6 +232,11 @@ class Body:
             for yi in range(self.y1 - self.y0):
                 L.append(f"    PIN8(acc[{yi}]);")
             L.append("    }")
+            if READ_LATE and u + 1 < len(units):
+                # the next unit's words are read after this unit's XORs (its words are dead
+                # then): the two banks are never live together
+                L.append("    __builtin_amdgcn_sched_barrier(0);")
+                read_unit(u + 1, nxt)
         return "\n".join(L)
 
     def window_step(self, x, cur):
@@ -300,28 +308,24 @@ _SCHED = {}
 _CACHE = os.path.join(ROOT, "shorthair_amd", "csrc", "gen_cache", "xor_sched.json")
 
 
-def unit_steps(R):
-    """Steps per XOR program for a ring of R slots: pairs need the two slots of the unit being
-    prefetched plus DMA in flight beyond the waited group (R >= 8); the (28,4) ring has 4."""
-    return 2 if JOINT == 2 and R >= 8 else 1
+def unit_steps(R, rows):
+    """Steps per XOR program for a ring of R slots and parts of `rows` rows: pairs need the two
+    slots of the unit being prefetched plus DMA in flight beyond the waited group (R >= 8; the
+    (28,4) ring has 4), and registers: 8 accumulators per row + the pair's 16 words + its ~20
+    live intermediates fit 128 VGPRs up to 8 rows ((190,66)'s 9-row parts spill with pairs; a
+    scratch spill's vmcnt wait would also drain the DMA ring)."""
+    return 2 if JOINT == 2 and R >= 8 and rows <= 8 else 1
 
 
 def _sched_key(tg, nbits):
     return f"{nbits}:" + ",".join(f"{t:x}" for t in tg)
 
 
-def _sched_compute(key):
-    import xor_sched
-    nbits, body = key.split(":")
-    tg = [int(t, 16) for t in body.split(",")]
-    inters, reps, _ = (xor_sched.schedule_joint(tg, int(nbits)) if int(nbits) > 8 else xor_sched.schedule(tg))
-    return key, ([[int(w), [int(o) for o in ops]] for w, ops in inters], {str(t): list(r) for t, r in reps.items()})
-
-
 def sched(tg, nbits):
     key = _sched_key(tg, nbits)
     if key not in _SCHED:
-        _SCHED[key] = _sched_compute(key)[1]
+        import xor_sched
+        _SCHED[key] = xor_sched.compute_key(key)[1]
     inters, reps = _SCHED[key]
     return [(w, tuple(ops)) for w, ops in inters], {int(t): tuple(r) for t, r in reps.items()}
 
@@ -350,7 +354,7 @@ def prefetch_schedules(cfgs):
     for k, m in cfgs:
         rows = generator(k, m)
         P, _, R = shape(k, m)[:3]
-        J = unit_steps(R)
+        J = unit_steps(R, -(-m // P))
         base, extra = divmod(m, P)
         y0 = 0
         for p in range(P):
@@ -366,8 +370,9 @@ def prefetch_schedules(cfgs):
     todo = sorted(k for k in keys if k not in _SCHED)
     if todo:
         import multiprocessing as mp
+        import xor_sched
         with mp.get_context("fork").Pool(max(1, min(16, os.cpu_count() or 1))) as pool:
-            for key, val in pool.imap_unordered(_sched_compute, todo, chunksize=8):
+            for key, val in pool.imap_unordered(xor_sched.compute_key, todo, chunksize=8):
                 _SCHED[key] = val
         save_sched_cache()
 
@@ -438,7 +443,7 @@ def gen_config(k, m):
     for mode in ("enc", "dec"):
         steps = [("c", x) for x in range(k)] + ([("r", y) for y in range(m)] if mode == "dec" else [])
         for p, (y0, y1) in enumerate(parts):
-            body = Body(k, rows, y0, y1).emit(R, sync, steps, KP)
+            body = Body(k, rows, y0, y1, max(b - a for a, b in parts)).emit(R, sync, steps, KP)
             nr = y1 - y0
             out.append(f"template <class Src, class Snk>")
             out.append(f"__device__ __forceinline__ void run_{name}_{mode}_p{p}(const Src &src, const Snk &sink) {{")

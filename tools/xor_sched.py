@@ -160,6 +160,15 @@ def schedule_joint(targets, nbits):
     return inters, reps, cur + len(inters)
 
 
+def compute_key(key):
+    """Cache entry of tools/gen_fixed_kernels.py: key "nbits:hex,hex,..." -> (key, JSON-able
+    (intermediates, representations)). A module-level function so a process pool can run it."""
+    nbits, body = key.split(":")
+    tg = [int(t, 16) for t in body.split(",")]
+    inters, reps, _ = schedule_joint(tg, int(nbits)) if int(nbits) > 8 else schedule(tg)
+    return key, ([[int(w), [int(o) for o in ops]] for w, ops in inters], {str(t): list(r) for t, r in reps.items()})
+
+
 def window_cost(targets):
     """Op count of the reference-style window tables (what the generator emitted before)."""
     have = set()
