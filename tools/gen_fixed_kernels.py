@@ -2,21 +2,24 @@
 """Generate compile-time-scheduled bitmatrix kernels: shorthair_amd/csrc/gen/fixed_k<k>_m<m>.hip.
 
 For a fixed (k, m) the generator matrix is a constant (reference cauchy_matrix(),
-cauchy_256.cpp:423-481, depends only on k and m), so every XOR of the windowed bitmatrix product
-(reference win_encode, cauchy_256.cpp:1398-1477) can be scheduled at build time: the table index
-of each lookup becomes a register name instead of a runtime value. That turns each output
-sub-block row update into ONE v_bitop3_b32 (a ^ T0[lo] ^ T1[hi]) with no index arithmetic --
-measured 8.7x cheaper than hipcc's s_set_gpr_idx lowering of a runtime-indexed table.
-Every XOR is emitted as a bitop3 intrinsic (X2 = truth table 0x3C for a 2-input XOR): plain `^`
-chains spanning all k steps are reassociated by LLVM into trees that keep every loaded word live
-(256 VGPRs + AGPR spills even at k=28).
+cauchy_256.cpp:423-481, depends only on k and m), so the whole bitmatrix product (reference
+win_encode, cauchy_256.cpp:1398-1477) can be scheduled at build time with every operand a
+register name. The reference's 4-bit window method costs 22 table XORs + one 3-input XOR per
+output row per input block (86 per 8-row part and block). Round 4 replaces it with straight-line
+XOR programs found by a greedy shortest-linear-program search (tools/xor_sched.py) over UNITS of
+two consecutive input blocks: a 3-input XOR can then take one word of each block, so most output
+rows cost one op per two blocks, plus ~14 shared intermediates per block -- ~62 ops per part and
+block at (200, 32) (VALU per launch 3.94e8 -> 3.0e8). Every XOR is emitted as a bitop3 intrinsic
+(X3 = truth table 0x96) or a 2-input `^` / v_xor_b32 asm (XV): plain `^` chains spanning all k
+steps are reassociated by LLVM into trees that keep every loaded word live (256 VGPRs + AGPR
+spills even at k=28).
 
 One generated kernel serves two modes (template flag DEC):
   encode       recovery[g][y] = sum_x M(C[y][x]) data[g][x]             (y < m, row 0 = ones)
   decode A     residual[g][y] = R_y + sum_{x received} M(C[y][x]) d_x   (erased x read as zeros;
                R_y streamed through the same ring as m extra steps after the k input steps)
-Rows are split into parts of <= 16 rows (128 accumulator VGPRs); the waves of one workgroup
-run the parts of the same columns, so the second part's loads hit L1/L2.
+Rows are split into parts of <= 9 rows (<= 72 accumulator VGPRs); the waves of one workgroup
+run the parts of the same columns and read the same LDS ring slots.
 
 Usage: python tools/gen_fixed_kernels.py            (all configs in CONFIGS)
 Run by shorthair_amd/build.py before compiling; the generated files are not committed.
@@ -305,7 +308,7 @@ class Body:
 # search costs ~0.1 s per 16-bit unit, ~2,600 units over CONFIGS.
 JOINT = int(os.environ.get("SH_JOINT", "2"))  # steps per XOR program; 0 = the reference's window tables
 _SCHED = {}
-_CACHE = os.path.join(ROOT, "shorthair_amd", "csrc", "gen_cache", "xor_sched.json")
+_CACHE = os.path.join(ROOT, "shorthair_amd", "csrc", "gen_cache", "xor_sched_v2.json")  # v2: 6-trial joint search
 
 
 def unit_steps(R, rows):

@@ -103,51 +103,52 @@ def _tri(n):
     return _TRI[n]
 
 
-def schedule_joint(targets, nbits):
+def schedule_joint(targets, nbits, trials=6, seed=0):
     """schedule() over nbits-bit targets (the 8-bit masks of `nbits // 8` consecutive steps
     packed, step j in bits 8j..8j+7): one accumulating op can then take a word of each step
     (acc ^ a_x ^ b_x+1), which the per-step form cannot. D is a dense 2^nbits table (nbits <=
-    16). Same return value as schedule()."""
+    16). The first trial breaks ties by the lowest candidate, the others at random (seeded:
+    the result is deterministic); the cheapest program wins (6 trials: ~4 % fewer ops than one).
+    Same return value as schedule()."""
     T = np.array([t for t in targets if t], np.int64)
     if T.size == 0:
         return [], {}, 0
     N = 1 << nbits
     idx = np.arange(N, dtype=np.int64)
-    avail = [1 << a for a in range(nbits)]
-    D = np.full(N, _BIG, np.int32)
-    D[0] = 0
-    front = np.zeros(1, np.int64)
-    d = 0
-    while front.size:  # BFS over sums of the inputs (popcount)
-        d += 1
-        nxt = np.unique((front[:, None] ^ np.array(avail, np.int64)[None, :]).ravel())
-        nxt = nxt[D[nxt] == _BIG]
-        D[nxt] = d
-        front = nxt
-    inters = []
-    cur = int(((D[T] + 1) // 2).sum())
-    while True:
-        A = np.array(avail, np.int64)
-        pi, ti = _tri(len(A))
-        c2 = A[pi[:, 0]] ^ A[pi[:, 1]]
-        c3 = A[ti[:, 0]] ^ A[ti[:, 1]] ^ A[ti[:, 2]]
-        C = np.unique(np.concatenate([c2, c3]))
-        C = C[D[C] > 1]
-        if C.size == 0:
-            break
-        newD = np.minimum(D[T][None, :], 1 + D[T[None, :] ^ C[:, None]])
-        cost = ((newD + 1) // 2).sum(axis=1) + 1  # the new word's own op
-        b = int(np.argmin(cost))
-        if cost[b] >= cur:
-            break
-        c = int(C[b])
-        hit = np.flatnonzero(c2 == c)
-        ops = tuple(int(v) for v in A[pi[hit[0]]]) if hit.size else \
-            tuple(int(v) for v in A[ti[np.flatnonzero(c3 == c)[0]]])
-        inters.append((c, ops))
-        avail.append(c)
-        D = np.minimum(D, 1 + D[idx ^ c])
+    D0 = np.array([bin(v).count("1") for v in range(N)], np.int32)  # sums of the inputs alone
+    rng = np.random.default_rng(seed)
+    best = None
+    for trial in range(trials):
+        avail = [1 << a for a in range(nbits)]
+        D = D0.copy()
+        inters = []
         cur = int(((D[T] + 1) // 2).sum())
+        while True:
+            A = np.array(avail, np.int64)
+            pi, ti = _tri(len(A))
+            c2 = A[pi[:, 0]] ^ A[pi[:, 1]]
+            c3 = A[ti[:, 0]] ^ A[ti[:, 1]] ^ A[ti[:, 2]]
+            C = np.unique(np.concatenate([c2, c3]))
+            C = C[D[C] > 1]
+            if C.size == 0:
+                break
+            newD = np.minimum(D[T][None, :], 1 + D[T[None, :] ^ C[:, None]])
+            cost = ((newD + 1) // 2).sum(axis=1) + 1  # the new word's own op
+            lo = int(cost.min())
+            if lo >= cur:
+                break
+            ties = np.flatnonzero(cost == lo)
+            c = int(C[ties[0] if trial == 0 else rng.choice(ties)])
+            hit = np.flatnonzero(c2 == c)
+            ops = tuple(int(v) for v in A[pi[hit[0]]]) if hit.size else \
+                tuple(int(v) for v in A[ti[np.flatnonzero(c3 == c)[0]]])
+            inters.append((c, ops))
+            avail.append(c)
+            D = np.minimum(D, 1 + D[idx ^ c])
+            cur = int(((D[T] + 1) // 2).sum())
+        if best is None or cur + len(inters) < best[2]:
+            best = (inters, avail, cur + len(inters), D)
+    inters, avail, total, D = best
     # representations: peel words greedily along D (each step removes one word, D drops by one)
     reps = {}
     for t in set(T.tolist()):
@@ -157,7 +158,7 @@ def schedule_joint(targets, nbits):
             rep.append(w)
             v ^= w
         reps[int(t)] = tuple(rep)
-    return inters, reps, cur + len(inters)
+    return inters, reps, total
 
 
 def compute_key(key):
@@ -165,7 +166,8 @@ def compute_key(key):
     (intermediates, representations)). A module-level function so a process pool can run it."""
     nbits, body = key.split(":")
     tg = [int(t, 16) for t in body.split(",")]
-    inters, reps, _ = schedule_joint(tg, int(nbits)) if int(nbits) > 8 else schedule(tg)
+    seed = int.from_bytes(__import__("hashlib").sha256(key.encode()).digest()[:8], "little")
+    inters, reps, _ = schedule_joint(tg, int(nbits), seed=seed) if int(nbits) > 8 else schedule(tg)
     return key, ([[int(w), [int(o) for o in ops]] for w, ops in inters], {str(t): list(r) for t, r in reps.items()})
 
 
