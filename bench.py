@@ -443,6 +443,8 @@ def _time_ops(args, sh, torch, s, k, m, B, G, data, rec, e_fixed, encode=True, i
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     te = td = 0.0
     for it in range(iters + 1):
+        if it == 1:
+            sh.profile(iters)  # stage times of the timed decodes (compile-time and tile paths)
         ev[0].record()
         if encode:
             assert sh.encode_batch(k, m, B, G, data, rec, s) == 0
@@ -453,6 +455,8 @@ def _time_ops(args, sh, torch, s, k, m, B, G, data, rec, e_fixed, encode=True, i
         if it:  # first pass warms up
             te += ev[0].elapsed_time(ev[1]) / iters
             td += ev[1].elapsed_time(ev[2]) / iters
+    stages = sh.profile_read()
+    sh.profile(0)
     g_chk = torch.arange(G, device="cuda")[:, None]
     ok = bool(torch.equal(ocnt.cpu(), torch.from_numpy(es).int()))
     if ok and e_fixed == emax:
@@ -461,6 +465,8 @@ def _time_ops(args, sh, torch, s, k, m, B, G, data, rec, e_fixed, encode=True, i
     r = {"decode_ms": round(td, 4), "decode_GBps": round(dec_b / td / 1e6, 1),
          "decode_frac": round(dec_b / td / 1e-3 / HBM_PEAK, 4), "mean_e": round(float(es.mean()), 2),
          "decode_ok": ok}
+    if stages:
+        r["decode_stages_ms"] = {"setup": round(stages[0], 4), "stageA": round(stages[1], 4), "stageB": round(stages[2], 4)}
     # work-normalized rate: the codec's work is one bitmatrix product of a B-byte block per
     # (input, output row) pair -- k*m per group for encode, k*m + e^2 for decode (stage A over all
     # m rows, stage B e x e) -- so "product_rate" = pairs x B / time in 1e15 byte-products per
