@@ -46,6 +46,7 @@
 
 #include "geometry.hpp"
 
+#include <algorithm>
 #include <type_traits>
 
 namespace sh {
@@ -128,6 +129,26 @@ __device__ __forceinline__ uint32_t col_off(int q, const Geometry &geo) {
     return 4u * q - (q >= geo.nq - 4 ? static_cast<uint32_t>(4 * geo.nq - geo.sub) : 0u);
 }
 
+// Per-lane geometry of the tile starting at column col0.
+template <class S>
+__device__ __forceinline__ WGInfo tile_info(int nq, long long col0, long long lo, long long hi) {
+    WGInfo w;
+    w.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    w.lane = threadIdx.x & 63;
+    const int cw = w.wave / S::P;
+    w.c = cw * 64 + w.lane;
+    w.col0 = col0;
+    w.lo = lo;
+    w.hi = hi;
+    w.g_first = static_cast<int>((col0 > lo ? col0 : lo) / nq);
+    const long long col = w.col0 + w.c;
+    w.valid = col >= lo && col < hi;
+    const int g = w.valid ? static_cast<int>(col / nq) : w.g_first;
+    w.q = static_cast<int>(col - static_cast<long long>(g) * nq);
+    w.gl = g - w.g_first;
+    return w;
+}
+
 template <class S, bool DEC>
 struct Src {
     static constexpr bool kStream = false;
@@ -139,6 +160,37 @@ struct Src {
     uint32_t rd;              // this lane's read offset in a slot (c * 4)
     const uint8_t *lds;       // ring base
     const uint8_t *pos;       // decode: [groups_per_wg][KP + MP] position tables (LDS)
+    // Persistent workgroups (encode): the next tile's source, whether there is one, and whether
+    // this tile's first NPF steps were already issued by the previous tile (`pref`).
+    __amdgpu_buffer_rsrc_t nrsrc;
+    uint32_t ndbase[S::DPW];
+    bool has_next = false, pref = false;
+    // uniform state (few SGPRs: the rest derives from k, B and the group count) to set up the
+    // next tile at the end of this one, so no per-lane state of the next tile is live across the
+    // body
+    const uint8_t *in_ptr;
+    long long next_col0;
+    int nq, groups;
+    const uint8_t *pos_g, *rpos_g;  // decode: the position tables in HBM (the next tile's are
+                                    // staged into the LDS copy at this tile's end)
+
+    __device__ __forceinline__ static void chunk_src(const Geometry &geo, long long in_gstride_, const WGInfo &w,
+                                                     uint32_t (&db)[S::DPW], int (&gl)[S::DPW]) {
+        const uint32_t gstride = static_cast<uint32_t>(in_gstride_);
+#pragma unroll
+        for (int j = 0; j < S::DPW; ++j) {
+            const int off = (w.wave * S::DPW + j) * 64 * S::W + w.lane * S::W;
+            const int aa = off / S::ROWB;
+            const int cc = (off - aa * S::ROWB) / 4;
+            const long long colx = w.col0 + cc;
+            const int gx = colx >= 0 ? static_cast<int>(colx / geo.nq) : -1;
+            const int qx = static_cast<int>(colx - static_cast<long long>(gx) * geo.nq);
+            gl[j] = gx - w.g_first;
+            db[j] = (colx >= w.lo && colx < w.hi)
+                        ? static_cast<uint32_t>(gx - w.g_first) * gstride + col_off(qx, geo) + aa * geo.sub
+                        : OOR;
+        }
+    }
 
     __device__ __forceinline__ void init(const FixedArgs &a, const WGInfo &w, const uint8_t *lds_ring,
                                          const uint8_t *lds_pos) {
@@ -150,34 +202,103 @@ struct Src {
         pos = lds_pos;
         wave = w.wave;
         rd = static_cast<uint32_t>(w.c) * 4u;
-        const uint32_t gstride = static_cast<uint32_t>(a.in_gstride);
+        chunk_src(a.geo, a.in_gstride, w, dbase, dgl);
+        in_ptr = a.in;
+        nq = geo.nq;
+        groups = a.groups;
+        pos_g = a.pos;
+        rpos_g = a.rpos;
+    }
+
+    __device__ __forceinline__ void advance() {
+        rsrc = nrsrc;
 #pragma unroll
-        for (int j = 0; j < S::DPW; ++j) {
-            const int off = (w.wave * S::DPW + j) * 64 * S::W + w.lane * S::W;
-            const int aa = off / S::ROWB;
-            const int cc = (off - aa * S::ROWB) / 4;
-            const long long colx = w.col0 + cc;
-            const int gx = colx >= 0 ? static_cast<int>(colx / geo.nq) : -1;
-            const int qx = static_cast<int>(colx - static_cast<long long>(gx) * geo.nq);
-            dgl[j] = gx - w.g_first;
-            dbase[j] = (colx >= w.lo && colx < w.hi)
-                           ? static_cast<uint32_t>(gx - w.g_first) * gstride + col_off(qx, geo) + aa * geo.sub
-                           : OOR;
-        }
+        for (int j = 0; j < S::DPW; ++j) dbase[j] = ndbase[j];
+        pref = true;
     }
 
     // Wait until this wave's DMAs of steps <= T are done (I = steps issued so far), then join the
     // workgroup barrier. One asm statement: nothing is scheduled between the two. Waves that
-    // issue no DMA (NDMA < NW) only join the barrier: their vmcnt holds nothing but the previous
-    // tile's output stores, which nothing here needs to wait for.
-    template <int T, int I>
+    // issue no DMA (NDMA < NW) only join the barrier: their vmcnt holds nothing but output
+    // stores, which nothing here needs to wait for. EX: vector-memory ops issued between the DMA
+    // of step T and the later ones when this tile's first steps were prefetched (the previous
+    // tile's epilogue stores, issued after its prefetch of steps < NPF): vmcnt counts them too.
+    template <int T, int I, int EX = 0>
     __device__ __forceinline__ void wait() const {
         constexpr int N = (I - T - 1) * S::DPW;
-        static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+        static_assert(N >= 0 && N + EX < 64, "vmcnt is 6 bits");
         if (S::NDMA % S::NW != 0 && wave * S::DPW >= S::NDMA)
             asm volatile("s_barrier" ::: "memory");
+        else if (EX != 0 && pref)
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N + EX) : "memory");
         else
             asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+    }
+
+    // Persistent encode, right after the last step's ring reads (release()): the next tile's
+    // steps 0..NP-1 into slots 0..NP-1 (free: every wave is past this tile's steps; the row
+    // images of the epilogue use the ring's top 2P slots), so their HBM latency runs under this
+    // tile's epilogue stores.
+    // Decode: the next tile's steps read their DMA sources through its position tables, staged
+    // into the LDS copy first (the current tile's are dead once its last step is read). Nothing
+    // else is outstanding in vmcnt here (the last ring wait was vmcnt(0), the stores come later),
+    // so waiting for these loads costs one load latency, still under the epilogue.
+    __device__ __forceinline__ void stage_pos(int g_first) const {
+        const int ghi = groups;
+        const int ngwg = (S::COLS - 1) / nq + 2;  // FixedArgs::groups_per_wg (launch_shape)
+        constexpr int TW = (S::KP + S::MP) / 4;
+        for (int i = threadIdx.x; i < ngwg * TW; i += S::NT) {  // one or two dwords per thread
+            const int lg = i / TW, t = i - lg * TW;
+            const int gg = g_first + lg;
+            uint32_t v = 0xFFFFFFFFu;
+            if (gg < ghi)
+                v = (t < S::KP / 4)
+                        ? reinterpret_cast<const uint32_t *>(pos_g + gg * static_cast<long long>(S::KP))[t]
+                        : reinterpret_cast<const uint32_t *>(rpos_g + gg * static_cast<long long>(S::MP))[t - S::KP / 4];
+            reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(pos))[i] = v;
+        }
+        __syncthreads();
+    }
+
+    __device__ __forceinline__ void prefetch_next(int np) const {
+        if (!has_next) return;
+        auto *self = const_cast<Src *>(this);
+        {  // the next tile's source, computed here: nothing of it is live across the body
+            const long long gstride = static_cast<long long>(S::K) * B;
+            const WGInfo w = tile_info<S>(nq, next_col0, 0, static_cast<long long>(groups) * nq);
+            self->nrsrc = wg_rsrc(in_ptr, gstride * groups, gstride, w.g_first);
+            Geometry g;
+            g.B = static_cast<int>(B);
+            g.sub = static_cast<int>(sub);
+            g.nq = nq;
+            g.tail = 4;
+            chunk_src(g, gstride, w, self->ndbase, self->dgl);
+            if (DEC) stage_pos(w.g_first);
+        }
+#pragma unroll
+        for (int t = 0; t < np; ++t) {
+            uint8_t *slot = const_cast<uint8_t *>(lds) + (t % S::R) * S::SLOT;
+            const Pre pr = pre(t);
+#pragma unroll
+            for (int j = 0; j < S::DPW; ++j) {
+                if (S::NDMA % S::NW != 0 && wave * S::DPW + j >= S::NDMA) break;  // uniform
+                lds_void *dst = (lds_void *)(slot + (wave * S::DPW + j) * 64 * S::W);
+                if (DEC) {
+                    const int p = pr.p[j];
+                    const uint32_t o = (p == 0xFF || ndbase[j] == OOR) ? OOR : ndbase[j] + static_cast<uint32_t>(p) * B;
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(nrsrc, dst, S::W, o, 0, 0, SH_LOAD_AUX);
+                } else {
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(nrsrc, dst, S::W, ndbase[j],
+                                                             static_cast<uint32_t>(t) * B, 0, SH_LOAD_AUX);
+                }
+            }
+        }
+    }
+
+    // Persistent encode, a prefetched tile: every wave has finished reading the previous tile's
+    // row images (ring's top slots) before this tile's DMAs refill them.
+    __device__ __forceinline__ void images_done() const {
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
 
     // After the last step: every wave's reads of the ring are done before any wave writes its
@@ -311,25 +432,47 @@ struct StreamSrc {
 template <class S>
 struct RowSink {
     __amdgpu_buffer_rsrc_t rsrc;
-    uint32_t gdst[2];         // per piece: destination offset without the row term (OOR: none)
-    uint32_t lsrc[2];         // per piece: byte offset inside a row image
-    uint32_t wofs;            // this lane's word in a row image (tile column * 4)
+    mutable uint32_t gdst[2];  // per piece: destination offset without the row term (OOR: none)
+    mutable uint32_t lsrc[2];  // per piece: byte offset inside a row image
+    mutable uint32_t wofs;     // this lane's word in a row image (tile column * 4)
     uint32_t B;
-    uint8_t *img;             // this part's row image, even rows (odd rows: + P * SLOT)
+    uint8_t *img;              // this part's row image, even rows (odd rows: + P * SLOT)
+    // uniform state (SGPRs): prepare() derives the per-lane offsets at the epilogue, so they
+    // are not live across the body
+    long long col0, lo, hi;
+    uint32_t out_gstride;
+    int g_first, nq, sub;
 
-    __device__ __forceinline__ void init(const FixedArgs &a, const WGInfo &w, int part, uint8_t *lds) {
-        const Geometry &geo = a.geo;
+    // img_slot: first ring slot of the images (persistent encode: the ring's top 2P slots, so the
+    // next tile's prefetched steps 0..R-2P-1 stay intact)
+    __device__ __forceinline__ void init(const FixedArgs &a, const WGInfo &w, int part, uint8_t *lds,
+                                         int img_slot = 0) {
         rsrc = wg_rsrc(a.out, a.out_bytes, a.out_gstride, w.g_first);
-        B = geo.B;
-        wofs = static_cast<uint32_t>(w.c) * 4u;
-        img = lds + part * S::SLOT;
-        const int nq = geo.nq;
-        const long long cs = w.col0 > w.lo ? w.col0 : w.lo;
-        const long long ce = w.col0 + S::COLS < w.hi ? w.col0 + S::COLS : w.hi;
-        const int cw = w.c >> 6;
+        B = a.geo.B;
+        img = lds + (img_slot + part) * S::SLOT;
+        col0 = w.col0;
+        lo = w.lo;
+        hi = w.hi;
+        out_gstride = static_cast<uint32_t>(a.out_gstride);
+        g_first = w.g_first;
+        nq = a.geo.nq;
+        sub = a.geo.sub;
+    }
+    // Per-lane piece offsets of the tile (called right before the first row).
+    __device__ __forceinline__ void prepare() const {
+        const int lane = threadIdx.x & 63;
+        const int cw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) / S::P;
+        wofs = static_cast<uint32_t>(cw * 64 + lane) * 4u;
+        const long long cs = col0 > lo ? col0 : lo;
+        const long long ce = col0 + S::COLS < hi ? col0 + S::COLS : hi;
+        Geometry geo;
+        geo.B = static_cast<int>(B);
+        geo.sub = sub;
+        geo.nq = nq;
+        geo.tail = 4;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            int rem = (cw * 2 + h) * 64 + w.lane;  // piece index in memory order
+            int rem = (cw * 2 + h) * 64 + lane;  // piece index in memory order
             gdst[h] = OOR;
             lsrc[h] = 0;
             for (long long g = cs / nq; g * nq < ce; ++g) {  // groups overlapping the tile
@@ -338,9 +481,9 @@ struct RowSink {
                 const int nch = (qb - qa) >> 2;  // whole chunks: tile and group edges are multiples of 4
                 if (rem < 8 * nch) {
                     const int b = rem / nch, q = qa + 4 * (rem - b * nch);
-                    gdst[h] = static_cast<uint32_t>(g - w.g_first) * static_cast<uint32_t>(a.out_gstride) +
+                    gdst[h] = static_cast<uint32_t>(g - g_first) * out_gstride +
                               col_off(q, geo) + static_cast<uint32_t>(b * geo.sub);
-                    lsrc[h] = static_cast<uint32_t>(b * S::ROWB) + static_cast<uint32_t>(g * nq + q - w.col0) * 4u;
+                    lsrc[h] = static_cast<uint32_t>(b * S::ROWB) + static_cast<uint32_t>(g * nq + q - col0) * 4u;
                     break;
                 }
                 rem -= 8 * nch;
@@ -371,23 +514,11 @@ struct RowSink {
 // non-inlined body took `src` by reference through scratch and read the LDS ring with flat loads.
 template <class S, bool DEC, class SrcT>
 __device__ __forceinline__ int kernel_prologue(const FixedArgs &a, uint8_t *lds, SrcT &src,
-                                               RowSink<S> &sink, long long col0, long long lo, long long hi) {
-    WGInfo w;
-    w.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    w.lane = threadIdx.x & 63;
+                                               RowSink<S> &sink, long long col0, long long lo, long long hi,
+                                               int img_slot = 0) {
+    const WGInfo w = tile_info<S>(a.geo.nq, col0, lo, hi);
     const int part = w.wave % S::P;
-    const int cw = w.wave / S::P;
-    w.c = cw * 64 + w.lane;
-    w.col0 = col0;
-    w.lo = lo;
-    w.hi = hi;
     const int nq = a.geo.nq;
-    w.g_first = static_cast<int>((col0 > lo ? col0 : lo) / nq);
-    const long long col = w.col0 + w.c;
-    w.valid = col >= lo && col < hi;
-    const int g = w.valid ? static_cast<int>(col / nq) : w.g_first;
-    w.q = static_cast<int>(col - static_cast<long long>(g) * nq);
-    w.gl = g - w.g_first;
     // The row images of the epilogue alias the start of the ring: they are used only after the
     // last step, behind Src::release()'s barrier, so the ring gets that LDS as extra slots.
     uint8_t *lds_pos = lds + (SrcT::kStream ? 2 * S::P * S::SLOT : S::R * S::SLOT);
@@ -409,7 +540,7 @@ __device__ __forceinline__ int kernel_prologue(const FixedArgs &a, uint8_t *lds,
         __syncthreads();
     }
     src.init(a, w, lds, lds_pos);
-    sink.init(a, w, part, lds);
+    sink.init(a, w, part, lds, img_slot);
     return part;  // the generated body issues the ring's first DMAs
 }
 
@@ -428,7 +559,51 @@ __device__ __forceinline__ int xcd_tile(int b, int n) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
 
-template <class S, bool DEC, bool STREAM = false>
+// Persistent encode workgroups: two per CU (the LDS ring and the registers allow two), each
+// walking tiles v = blockIdx.x + i * grid in xcd_tile order (grid % 8 == 0, so every tile of a
+// workgroup lies on its XCD and the 64 workgroups of an XCD code 64 neighbouring tiles at a time,
+// as the one-tile grid does). A tile prefetches its successor's first NPF steps right after its
+// last step, so their HBM latency runs under its epilogue stores instead of opening the next
+// tile with an empty ring (round-4 lab: the first ring wait of a fresh tile took 9.2 us of a
+// 109 us tile).
+// Tile loop of a persistent workgroup; RUN(part, src, sink) is the generated body (a macro, so
+// the ~15K-instruction body is inlined: called as a function it would take `src` through
+// scratch, and a scratch load's vmcnt wait drains the ring).
+#define SH_PERSISTENT_TILES(S, DEC, RUN)                                                          \
+    do {                                                                                          \
+        const long long hi_ = static_cast<long long>(a.groups) * a.geo.nq;                        \
+        const int ntiles_ = static_cast<int>((hi_ + S::COLS - 1) / S::COLS);                      \
+        int v_ = blockIdx.x;                                                                      \
+        if (v_ >= ntiles_) break;                                                                 \
+        Src<S, DEC> src;                                                                          \
+        RowSink<S> sink;                                                                          \
+        const int part = kernel_prologue<S, DEC>(a, lds, src, sink,                               \
+                                                 static_cast<long long>(xcd_tile(v_, ntiles_)) * S::COLS, 0, \
+                                                 hi_, S::R - 2 * S::P);                           \
+        for (;;) {                                                                                \
+            const int vn_ = v_ + static_cast<int>(gridDim.x);                                     \
+            src.has_next = vn_ < ntiles_;                                                         \
+            src.next_col0 = static_cast<long long>(xcd_tile(src.has_next ? vn_ : v_, ntiles_)) * S::COLS; \
+            RUN(part, src, sink);                                                                 \
+            if (!src.has_next) break;                                                             \
+            v_ = vn_;                                                                             \
+            const WGInfo w_ = tile_info<S>(a.geo.nq, src.next_col0, 0, hi_);                      \
+            src.advance();                                                                        \
+            sink.init(a, w_, part, lds, S::R - 2 * S::P);                                         \
+        }                                                                                         \
+    } while (0)
+
+inline int persistent_slots() {
+    static const int cus = [] {
+        int d = 0, n = 0;
+        if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+            n = 256;
+        return n > 0 ? n : 256;
+    }();
+    return 2 * cus;  // a multiple of 8 on MI355X (256 CUs)
+}
+
+template <class S, bool DEC, bool STREAM = false, bool PERS = false>
 inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArgs)) {
     constexpr bool dec = DEC;
     a.groups_per_wg = (S::COLS - 1) / a.geo.nq + 2;
@@ -437,7 +612,8 @@ inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArg
     static_assert(STREAM || 2 * S::P <= S::R, "row images must fit inside the ring");
     const size_t lds = front + (dec ? static_cast<size_t>(a.groups_per_wg) * (S::KP + S::MP) : 0);
     const long long cols = static_cast<long long>(a.groups) * a.geo.nq;
-    const unsigned blocks = static_cast<unsigned>((cols + S::COLS - 1) / S::COLS);  // one tile each
+    unsigned blocks = static_cast<unsigned>((cols + S::COLS - 1) / S::COLS);  // one tile each
+    if (PERS) blocks = std::min<unsigned>(blocks, static_cast<unsigned>(persistent_slots()));
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(S::NT), lds, s, a);
     return hipGetLastError();
 }
@@ -464,6 +640,22 @@ inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArg
     }                                                                                             \
     hipError_t launch_##NAME##_##MODE(FixedArgs a, hipStream_t s) {                               \
         return launch_shape<Shape<K, M, P, CW, R, DMA>, DEC, STREAM>(a, s, kern_##NAME##_##MODE); \
+    }                                                                                             \
+    }                                                                                             \
+    }
+
+// The persistent form (SH_PERSISTENT_TILES above): two workgroups per CU walk the
+// tiles, each tile prefetching its successor's first steps.
+#define FIXED_KERNEL_PERSISTENT(NAME, K, M, P, CW, R, MINW, MODE, DEC)                            \
+    namespace sh {                                                                                \
+    namespace fixed {                                                                             \
+    __global__ __launch_bounds__(64 * CW * P, MINW) void kern_##NAME##_##MODE(FixedArgs a) {      \
+        extern __shared__ __attribute__((aligned(16))) uint8_t lds[];                             \
+        using S = Shape<K, M, P, CW, R, true>;                                                    \
+        SH_PERSISTENT_TILES(S, DEC, run_##NAME##_##MODE);                                         \
+    }                                                                                             \
+    hipError_t launch_##NAME##_##MODE(FixedArgs a, hipStream_t s) {                               \
+        return launch_shape<Shape<K, M, P, CW, R, true>, DEC, false, true>(a, s, kern_##NAME##_##MODE); \
     }                                                                                             \
     }                                                                                             \
     }

@@ -555,21 +555,28 @@ __global__ __launch_bounds__(64 * NW) void stageb_v2(StageBV2Args a) {
     const int ncols = min(64, geo.nq - c0);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
+    const int j0 = (blockIdx.y * NW + wave) * 8;
+    // The prologue's loads do not depend on e (a scalar load of its own): the row list and this
+    // wave's coefficient bytes are loaded for emax rows at once (entries past e are in the
+    // group's workspace, unused), so e, the rows and the coefficients take one memory latency
+    // together, the ring DMAs the next; loaded one after the other (each waiting for the last)
+    // they took four.
+    // the group's compacted residual-row list, 4 rows per lane (readlane by the issuing waves)
+    uint32_t rrv;
+    __builtin_memcpy(&rrv, a.rrow + static_cast<long long>(g) * a.ldR + 4 * (4 * lane < a.ldR ? lane : 0), 4);
+    // this wave's coefficient bytes S^-1[j0..j0+7][i], i < emax (transposed table [i][j]: 8
+    // contiguous bytes per row); rows 2l and 2l+1 per lane, written to LDS after the DMA issue
+    constexpr int CFL = (2 * MAXE + 63) / 64;  // loads per lane
+    const uint8_t *cg = a.coefT + static_cast<long long>(g) * a.coefT_gstride + (j0 < a.ldT ? j0 : 0);
+    uint32_t cfw[CFL];
+#pragma unroll
+    for (int u = 0; u < CFL; ++u) {
+        const int i = lane + 64 * u < 2 * a.emax ? lane + 64 * u : 0;  // unconditional: a static vmcnt
+        __builtin_memcpy(&cfw[u], cg + static_cast<long long>(i >> 1) * a.ldT + 4 * (i & 1), 4);
+    }
     const int e = a.e[g];
     if (e <= 0) return;  // uniform over the workgroup
-    const int j0 = (blockIdx.y * NW + wave) * 8;
     const bool active = j0 < e;
-    // this wave's coefficient bytes S^-1[j0..j0+7][i], i < e (transposed table [i][j]: 8
-    // contiguous bytes per row), into LDS; rows 2l and 2l+1 per lane
-    const uint8_t *cg = a.coefT + static_cast<long long>(g) * a.coefT_gstride + j0;
-    for (int i = lane; i < 2 * e && active; i += 64) {
-        uint32_t w;
-        __builtin_memcpy(&w, cg + static_cast<long long>(i >> 1) * a.ldT + 4 * (i & 1), 4);
-        cf[wave][i >> 1][i & 1] = w;
-    }
-    // the group's compacted residual-row list, 4 rows per lane (readlane by the issuing waves)
-    uint32_t rrv = 0;
-    if (4 * lane < e) __builtin_memcpy(&rrv, a.rrow + static_cast<long long>(g) * a.ldR + 4 * lane, 4);
     const long long gbase = static_cast<long long>(g) * a.in_gstride;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.in + gbase), static_cast<short>(0), static_cast<int>(a.in_gstride), 0x00020000);
@@ -602,6 +609,11 @@ __global__ __launch_bounds__(64 * NW) void stageb_v2(StageBV2Args a) {
     uint32_t z0 = 0, z1 = 0;
     const uint32_t lo = static_cast<uint32_t>(a.snip_base), hi = static_cast<uint32_t>(a.snip_base >> 32);
     for (int i = 0; i < RB_R - RB_S; ++i) issue(i);
+#pragma unroll
+    for (int u = 0; u < CFL; ++u) {
+        const int i = lane + 64 * u;
+        if (i < 2 * e && active) cf[wave][i >> 1][i & 1] = cfw[u];
+    }
     const int ngroups = (e + RB_S - 1) / RB_S;
     for (int ig = 0; ig < ngroups; ++ig) {
         // own DMAs of rows RB_S*ig.. landed (RB_R - 2 * RB_S younger ones may be outstanding);

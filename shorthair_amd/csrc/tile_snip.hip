@@ -282,6 +282,7 @@ __device__ __forceinline__ void step_col(const uint32_t (&d)[8], uint32_t g0, ui
 // Every wave joins one barrier per row of a part (8), storing its part's rows < nr.
 template <int YI, class Snk>
 __device__ __forceinline__ void store_rows(const Snk &sink, int nr, int y0, const uint32_t (&acc)[8][8]) {
+    if constexpr (YI == 0) sink.prepare();  // per-lane piece offsets, derived at the epilogue
     if constexpr (YI < 8) {
         if (YI < nr)
             sink.template row<YI>(y0 + YI, acc[YI]);

@@ -140,7 +140,7 @@ class Body:
         have.add(name)
         return name
 
-    def emit(self, R, S, steps, KP):
+    def emit(self, R, S, steps, KP, npf=0, st=0):
         """Software-pipelined units (see fixed_common.hpp). A unit is JOINT consecutive input
         steps (a pair by default; recovery-row steps are single units) computed as one XOR
         program (tools/xor_sched.py); while unit u computes, the words of unit u+1 are read from
@@ -149,7 +149,10 @@ class Body:
         next S steps and joins the workgroup barrier; every wave is then past the units before u,
         so the ring slots of their steps are free and are refilled (up to R steps ahead) right
         there. steps: ("c", x) = input column x (position-table entry x), ("r", y) = decode only:
-        the received recovery block of generator row y (entry KP + y), added to row y's residual."""
+        the received recovery block of generator row y (entry KP + y), added to row y's residual.
+        npf > 0 (persistent encode): a tile after the first finds its steps 0..npf-1 already
+        issued by its predecessor, followed by that tile's epilogue stores (st per wave), so
+        waits for steps < npf count st more outstanding operations there."""
         L = self.lines
         n = len(steps)
         dma = "nodma" not in ABLATE
@@ -178,13 +181,26 @@ class Body:
                     L.append(f"    src.read({t % R}, " + ", ".join(f"{bank}{8 * j + a}" for a in range(8)) + ");")
 
         nxt_issue = min(n, R - 1)  # steps 0..nxt_issue-1 issued (in order)
+        npf = min(npf, nxt_issue)
+
+        def wait(T, I):
+            ex = st if T < npf else 0
+            return f"    src.template wait<{T}, {I}, {ex}>();" if ex else f"    src.template wait<{T}, {I}>();"
         if dma:
-            for t in range(nxt_issue):
+            if npf:
+                L.append("    if (!src.pref) {")
+            for t in range(npf):
+                L.append(f"    src.issue({t}, src.pre({tidx(steps[t])}));")
+            if npf:
+                L.append("    } else {")
+                L.append("    src.images_done();")
+                L.append("    }")
+            for t in range(npf, nxt_issue):
                 L.append(f"    src.issue({t}, src.pre({tidx(steps[t])}));")
         need = units[1][-1] if len(units) > 1 else units[0][-1]
         landed = min(n - 1, max(need, S - 1), nxt_issue - 1)
         assert need <= landed
-        L.append(f"    src.template wait<{landed}, {nxt_issue}>();")
+        L.append(wait(landed, nxt_issue))
         read_unit(0, "dA")
         if nxt_issue < n:
             L.append(f"    typename Src::Pre pre = src.pre({tidx(steps[nxt_issue])});")
@@ -202,7 +218,7 @@ class Body:
                     landed = min(n - 1, nu[-1] + S - 1, nxt_issue - 1)
                     assert nu[-1] <= landed, "ring too small for the unit size"
                     if "nobar" not in ABLATE:
-                        L.append(f"    src.template wait<{landed}, {nxt_issue}>();")
+                        L.append(wait(landed, nxt_issue))
                     while nxt_issue < n and nxt_issue - R <= unit[0] - 1:
                         if dma:
                             L.append(f"    src.issue({nxt_issue}, pre);")
@@ -415,6 +431,20 @@ def shape(k, m):
     return P, CW, R, minw, sync
 
 
+PERSIST = os.environ.get("SH_PERSIST", "0") == "1"
+
+
+PERSIST_DEC = os.environ.get("SH_PERSIST_DEC", "1") == "1"
+
+
+def persistent(mode, P, R):
+    """Persistent workgroups with next-tile prefetch (fixed_common.hpp SH_PERSISTENT_TILES) for
+    kernels whose ring keeps >= 4 slots below the 2P row images; decode stage A stages the next
+    tile's position tables into LDS at the end of each tile."""
+    return (PERSIST and (mode == "enc" or PERSIST_DEC) and not stream_mode(P) and R - 2 * P >= 4
+            and "nodma" not in ABLATE)
+
+
 def stream_mode(P):
     """One-part shapes may load each lane's words straight into registers (StreamSrc in
     fixed_common.hpp) instead of through the LDS ring."""
@@ -443,10 +473,14 @@ def gen_config(k, m):
            "namespace fixed {",
            ""]
     KP = (k + 3) & ~3
+    pers = {mode: persistent(mode, P, R) for mode in ("enc", "dec")}
     for mode in ("enc", "dec"):
         steps = [("c", x) for x in range(k)] + ([("r", y) for y in range(m)] if mode == "dec" else [])
         for p, (y0, y1) in enumerate(parts):
-            body = Body(k, rows, y0, y1, max(b - a for a, b in parts)).emit(R, sync, steps, KP)
+            # epilogue stores per wave: two 16-byte pieces per row of its part (RowSink::row)
+            npf = R - 2 * P if pers[mode] else 0
+            body = Body(k, rows, y0, y1, max(b - a for a, b in parts)).emit(R, sync, steps, KP, npf=npf,
+                                                                            st=2 * (y1 - y0))
             nr = y1 - y0
             out.append(f"template <class Src, class Snk>")
             out.append(f"__device__ __forceinline__ void run_{name}_{mode}_p{p}(const Src &src, const Snk &sink) {{")
@@ -458,6 +492,9 @@ def gen_config(k, m):
             out.append("    __builtin_amdgcn_sched_barrier(0);")
             out.append(f"    // epilogue: store rows {y0}..{y1 - 1}")
             out.append("    src.release();  // the store scratch aliases the ring")
+            if pers[mode]:
+                out.append(f"    src.prefetch_next({R - 2 * P});  // the next tile's first steps")
+            out.append("    sink.prepare();")
             nrmax = max(b - a for a, b in parts)
             for yi in range(nrmax):  # every part joins the same number of row barriers
                 out.append("    __builtin_amdgcn_sched_barrier(0);")
@@ -496,8 +533,9 @@ def gen_config(k, m):
         with open(path, "w") as f:
             f.write(f"// GENERATED by tools/gen_fixed_kernels.py -- do not edit. (k={k}, m={m}, {mode})\n"
                     f'#include "fixed_{name}.inc"\n'
-                    f"FIXED_KERNEL({name}, {k}, {m}, {P}, {CW}, {R}, {minw}, {mode}, {dec}, "
-                    f"{'false' if 'nodma' in ABLATE else 'true'}, {'true' if stream_mode(P) else 'false'})\n")
+                    + (f"FIXED_KERNEL_PERSISTENT({name}, {k}, {m}, {P}, {CW}, {R}, {minw}, {mode}, {dec})\n" if pers[mode] else
+                       f"FIXED_KERNEL({name}, {k}, {m}, {P}, {CW}, {R}, {minw}, {mode}, {dec}, "
+                       f"{'false' if 'nodma' in ABLATE else 'true'}, {'true' if stream_mode(P) else 'false'})\n"))
         paths.append(path)
     return paths
 
