@@ -13,6 +13,7 @@
 #include <cstring>
 #include <array>
 #include <atomic>
+#include <condition_variable>
 #include <memory>
 #include <map>
 #include <mutex>
@@ -99,6 +100,17 @@ struct TileLaunch {
     uint32_t hi;        // high dword of every snippet address of the launch
 };
 
+// Staging of one single-group call (cauchy_256_encode / cauchy_256_decode): pinned host and
+// device buffers and its own stream, so calls from different threads -- e.g. two Shorthair codec
+// objects -- copy and compute concurrently instead of queueing on one buffer and one stream. The
+// reference codec is reentrant per call (cauchy_256.cpp keeps no state beyond its init tables).
+struct StageSlot {
+    hipStream_t stream = nullptr;
+    PinnedBuf h;
+    DevBuf d;
+};
+constexpr size_t kMaxStageSlots = 8;  // concurrent single-group calls; more threads wait for a slot
+
 struct Context {
     std::mutex mu;          // guards lazy state (tables, caches, the stream map, profiling events)
     bool ready = false;
@@ -123,10 +135,11 @@ struct Context {
     // stage B, in a ring of `evq.size()` quadruples (no host synchronisation while recording)
     std::vector<std::array<hipEvent_t, 4>> evq;
     int ev_next = 0, ev_count = 0;
-    // single-group staging, guarded by stage_mu for the whole call
+    // single-group staging slots (SlotLease): a call holds one for its whole duration
     std::mutex stage_mu;
-    PinnedBuf h_stage;
-    DevBuf d_stage;
+    std::condition_variable stage_cv;
+    std::vector<std::unique_ptr<StageSlot>> stage_all;
+    std::vector<StageSlot *> stage_free;
 };
 
 Context &ctx() {
@@ -958,7 +971,8 @@ extern "C" int cauchy_256_sync(void *stream) {
 }
 
 // =============================================================================================
-// Drop-in single-group ABI (cauchy_256.h). One group per call through pinned staging.
+// Drop-in single-group ABI (cauchy_256.h). One group per call through a pinned staging slot with
+// its own stream (SlotLease): concurrent calls from different threads overlap on the GPU.
 // =============================================================================================
 // The reference's exported product/quotient tables (cauchy_256.cpp:346-347, built by GFC256Init
 // :349-386 on the first _cauchy_256_init): 256 x 256 bytes each, entry (y << 8) + x = x * y and
@@ -986,6 +1000,46 @@ void export_field_tables() {
 }
 }  // namespace
 
+namespace {
+// A staging slot for the duration of one call: a free one, a new one while fewer than
+// kMaxStageSlots exist, else the next one released. `rc` != 0: no slot (stream creation failed).
+struct SlotLease {
+    Context &c;
+    StageSlot *s = nullptr;
+    int rc = 0;
+    explicit SlotLease(Context &cx) : c(cx) {
+        std::unique_lock<std::mutex> lk(c.stage_mu);
+        for (;;) {
+            if (!c.stage_free.empty()) {
+                s = c.stage_free.back();
+                c.stage_free.pop_back();
+                return;
+            }
+            if (c.stage_all.size() < kMaxStageSlots) break;
+            c.stage_cv.wait(lk);
+        }
+        auto slot = std::make_unique<StageSlot>();
+        if (hipStreamCreateWithFlags(&slot->stream, hipStreamNonBlocking) != hipSuccess) {
+            std::fprintf(stderr, "libcauchy256: hipStreamCreateWithFlags failed\n");
+            rc = -2;
+            return;
+        }
+        s = slot.get();
+        c.stage_all.push_back(std::move(slot));
+    }
+    ~SlotLease() {
+        if (!s) return;
+        {
+            std::lock_guard<std::mutex> g(c.stage_mu);
+            c.stage_free.push_back(s);
+        }
+        c.stage_cv.notify_one();
+    }
+    SlotLease(const SlotLease &) = delete;
+    SlotLease &operator=(const SlotLease &) = delete;
+};
+}  // namespace
+
 extern "C" int _cauchy_256_init(int expected_version) {
     if (expected_version != CAUCHY_256_VERSION) return -1;  // reference cauchy_256.cpp:392-394
     export_field_tables();
@@ -1003,20 +1057,22 @@ extern "C" int cauchy_256_encode(int k, int m, const unsigned char *data_ptrs[],
     const int kin = k <= 1 ? 1 : k;
     const size_t in_bytes = static_cast<size_t>(kin) * block_bytes;
     const size_t out_bytes = static_cast<size_t>(m) * block_bytes;
-    std::lock_guard<std::mutex> g(c.stage_mu);  // one staging area; calls serialise like Shorthair's
-    const size_t scratch = 8 * out_bytes;      // step-slice partials (latency path)
-    if (int rc = c.h_stage.ensure(in_bytes + out_bytes)) return rc;
-    if (int rc = c.d_stage.ensure(in_bytes + out_bytes + scratch)) return rc;
-    uint8_t *h = static_cast<uint8_t *>(c.h_stage.p);
-    uint8_t *d = static_cast<uint8_t *>(c.d_stage.p);
+    SlotLease sl(c);
+    if (sl.rc) return sl.rc;
+    StageSlot &st = *sl.s;
+    const size_t scratch = 8 * out_bytes;  // step-slice partials (latency path)
+    if (int rc = st.h.ensure(in_bytes + out_bytes)) return rc;
+    if (int rc = st.d.ensure(in_bytes + out_bytes + scratch, st.stream)) return rc;
+    uint8_t *h = static_cast<uint8_t *>(st.h.p);
+    uint8_t *d = static_cast<uint8_t *>(st.d.p);
     for (int x = 0; x < kin; ++x) std::memcpy(h + static_cast<size_t>(x) * block_bytes, data_ptrs[x], block_bytes);
-    SH_CHECK(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, c.stream));
-    const int rc = encode_batch(k, m, block_bytes, 1, d, d + in_bytes, c.stream, d + in_bytes + out_bytes);
+    SH_CHECK(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, st.stream));
+    const int rc = encode_batch(k, m, block_bytes, 1, d, d + in_bytes, st.stream, d + in_bytes + out_bytes);
     if (rc == -2) return rc;
     // Like the reference, a rejected call has still written recovery row 0.
     const size_t copy = (rc == 0) ? out_bytes : static_cast<size_t>(block_bytes);
-    SH_CHECK(hipMemcpyAsync(h + in_bytes, d + in_bytes, copy, hipMemcpyDeviceToHost, c.stream));
-    SH_CHECK(hipStreamSynchronize(c.stream));
+    SH_CHECK(hipMemcpyAsync(h + in_bytes, d + in_bytes, copy, hipMemcpyDeviceToHost, st.stream));
+    SH_CHECK(hipStreamSynchronize(st.stream));
     std::memcpy(recovery_blocks, h + in_bytes, copy);
     return rc;
 }
@@ -1031,12 +1087,14 @@ extern "C" int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes) {
     }
     if (block_bytes <= 0) return 0;
     const size_t data_bytes = static_cast<size_t>(k) * block_bytes;
-    std::lock_guard<std::mutex> g(c.stage_mu);
+    SlotLease sl(c);
+    if (sl.rc) return sl.rc;
+    StageSlot &st = *sl.s;
     const size_t scratch = 8 * static_cast<size_t>(std::max(m, 1)) * block_bytes;  // step-slice partials
-    if (int rc = c.h_stage.ensure(data_bytes + 256 + 8)) return rc;
-    if (int rc = c.d_stage.ensure(data_bytes + 256 + scratch)) return rc;
-    uint8_t *h = static_cast<uint8_t *>(c.h_stage.p);
-    uint8_t *d = static_cast<uint8_t *>(c.d_stage.p);
+    if (int rc = st.h.ensure(data_bytes + 256 + 8)) return rc;
+    if (int rc = st.d.ensure(data_bytes + 256 + scratch, st.stream)) return rc;
+    uint8_t *h = static_cast<uint8_t *>(st.h.p);
+    uint8_t *d = static_cast<uint8_t *>(st.d.p);
     for (int i = 0; i < k; ++i) {
         std::memcpy(h + static_cast<size_t>(i) * block_bytes, blocks[i].data, block_bytes);
         h[data_bytes + i] = blocks[i].row;
@@ -1044,11 +1102,11 @@ extern "C" int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes) {
     // pinned word for the group's e, past the rows (the decode core fills it when it runs)
     int *e_host = reinterpret_cast<int *>(h + ((data_bytes + k + 3) & ~static_cast<size_t>(3)));
     *e_host = 0;
-    SH_CHECK(hipMemcpyAsync(d, h, data_bytes + k, hipMemcpyHostToDevice, c.stream));
-    const int rc = decode_batch(k, m, block_bytes, 1, d, d + data_bytes, c.stream, e_host, d + data_bytes + 256);
+    SH_CHECK(hipMemcpyAsync(d, h, data_bytes + k, hipMemcpyHostToDevice, st.stream));
+    const int rc = decode_batch(k, m, block_bytes, 1, d, d + data_bytes, st.stream, e_host, d + data_bytes + 256);
     if (rc != 0) return rc;
-    SH_CHECK(hipMemcpyAsync(h, d, data_bytes + k, hipMemcpyDeviceToHost, c.stream));
-    SH_CHECK(hipStreamSynchronize(c.stream));
+    SH_CHECK(hipMemcpyAsync(h, d, data_bytes + k, hipMemcpyDeviceToHost, st.stream));
+    SH_CHECK(hipStreamSynchronize(st.stream));
     const int e = *e_host;
     // A group with more recovery blocks than erasures (outside the reference's contract: its
     // rows would be duplicates) is left untouched and reported as invalid.

@@ -173,6 +173,8 @@ struct Src {
     int nq, groups;
     const uint8_t *pos_g, *rpos_g;  // decode: the position tables in HBM (the next tile's are
                                     // staged into the LDS copy at this tile's end)
+    uint32_t lbase;           // decode: this lane's column in its group (OOR: past the batch)
+    int lgl;                  // ... and its group (position-table index)
 
     __device__ __forceinline__ static void chunk_src(const Geometry &geo, long long in_gstride_, const WGInfo &w,
                                                      uint32_t (&db)[S::DPW], int (&gl)[S::DPW]) {
@@ -208,6 +210,19 @@ struct Src {
         groups = a.groups;
         pos_g = a.pos;
         rpos_g = a.rpos;
+        lgl = w.gl;
+        lbase = w.valid ? static_cast<uint32_t>(w.gl) * static_cast<uint32_t>(a.in_gstride) + col_off(w.q, geo) : OOR;
+    }
+
+    // Decode: residual row y starts as the received recovery block R_y (position entry KP + y;
+    // absent: zeros), loaded straight into the lane's 8 accumulators before the ring's first
+    // DMA, so stage A runs the k input steps only (no m extra ring steps). Older than every DMA,
+    // these loads are covered by the ring's counted waits; the compiler's own wait guards the use.
+    __device__ __forceinline__ void rrow(int y, uint32_t (&r)[8]) const {
+        const int p = pos[lgl * (S::KP + S::MP) + S::KP + y];
+        const uint32_t o = (p == 0xFF || lbase == OOR) ? OOR : lbase + static_cast<uint32_t>(p) * B;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) r[s] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, o + s * sub, 0, SH_LOAD_AUX);
     }
 
     __device__ __forceinline__ void advance() {
@@ -383,6 +398,12 @@ struct StreamSrc {
     }
     template <int T, int I>
     __device__ __forceinline__ void wait() const {}
+    __device__ __forceinline__ void rrow(int y, uint32_t (&r)[8]) const {  // as Src::rrow
+        const int p = pos[gl * (S::KP + S::MP) + S::KP + y];
+        const uint32_t o = (p == 0xFF || lane_base == OOR) ? OOR : lane_base + static_cast<uint32_t>(p) * B;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) r[s] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, o + s * sub, 0, SH_LOAD_AUX);
+    }
     __device__ __forceinline__ static void release() {
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }

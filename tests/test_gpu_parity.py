@@ -107,6 +107,48 @@ def test_single_group_decode_abi(sh, c):
     assert np.array_equal(out, vectors()[c["name"] + "_out"])
 
 
+def test_single_group_abi_concurrent(sh):
+    """Single-group calls from several threads at once (two Shorthair codec objects on two threads):
+    each call holds its own staging slot and stream, so the calls overlap and none sees another's
+    data. Every result is checked against the oracle."""
+    import threading
+    ora = po.oracle()
+    shapes = [(200, 32, 1400), (64, 16, 1400), (28, 4, 256), (12, 5, 64), (150, 40, 1352), (2, 2, 8)]
+    jobs = []
+    for t, (k, m, B) in enumerate(shapes):
+        data = po.fill_group(900 + t, k, B, 0x77)
+        rc, rec = ora.encode(k, m, data, B)
+        assert rc == 0
+        e = min(m, k)
+        rows = np.array(list(range(e, k)) + list(range(k, k + e)), np.uint8)
+        jobs.append((k, m, B, data, rec, rows))
+    errors = []
+
+    def worker(job, iters=12):
+        k, m, B, data, rec, rows = job
+        whole = np.concatenate([data, rec])
+        try:
+            for _ in range(iters):
+                out = np.zeros(m * B, np.uint8)
+                assert sh.cauchy_256_encode(k, m, [data[x].ctypes.data for x in range(k)], out.ctypes.data, B) == 0
+                assert np.array_equal(out.reshape(m, B), rec)
+                bufs = [whole[r].copy() for r in rows]
+                arr = (sh.Block * k)(*[sh.Block(b.ctypes.data, int(r)) for b, r in zip(bufs, rows)])
+                assert sh.cauchy_256_decode(k, m, arr, B) == 0
+                for i in range(k):
+                    assert np.array_equal(bufs[i], data[arr[i].row])
+        except Exception as ex:  # reported on the main thread
+            errors.append((k, m, B, repr(ex)))
+
+    threads = [threading.Thread(target=worker, args=(j,)) for j in jobs for _ in range(2)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=120)
+    assert not any(th.is_alive() for th in threads)
+    assert not errors, errors
+
+
 # ------------------------------------------------------------------------- batches vs oracle
 def _oracle_encode_groups(k, m, B, cfg, groups):
     ora = po.oracle()

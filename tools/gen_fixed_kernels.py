@@ -17,7 +17,7 @@ spills even at k=28).
 One generated kernel serves two modes (template flag DEC):
   encode       recovery[g][y] = sum_x M(C[y][x]) data[g][x]             (y < m, row 0 = ones)
   decode A     residual[g][y] = R_y + sum_{x received} M(C[y][x]) d_x   (erased x read as zeros;
-               R_y streamed through the same ring as m extra steps after the k input steps)
+               R_y loaded into the accumulators before the k input steps)
 Rows are split into parts of <= 9 rows (<= 72 accumulator VGPRs); the waves of one workgroup
 run the parts of the same columns and read the same LDS ring slots.
 
@@ -432,6 +432,9 @@ def shape(k, m):
 
 
 PERSIST = os.environ.get("SH_PERSIST", "0") == "1"
+# Decode stage A: residual rows start as the recovery blocks R_y, loaded into the accumulators in
+# the prologue (Src::rrow), instead of m extra ring steps (0: the ring steps, A/B only).
+RINIT = os.environ.get("SH_RINIT", "1") == "1"
 
 
 PERSIST_DEC = os.environ.get("SH_PERSIST_DEC", "1") == "1"
@@ -475,7 +478,8 @@ def gen_config(k, m):
     KP = (k + 3) & ~3
     pers = {mode: persistent(mode, P, R) for mode in ("enc", "dec")}
     for mode in ("enc", "dec"):
-        steps = [("c", x) for x in range(k)] + ([("r", y) for y in range(m)] if mode == "dec" else [])
+        rinit = mode == "dec" and RINIT and not pers[mode]
+        steps = [("c", x) for x in range(k)] + ([("r", y) for y in range(m)] if mode == "dec" and not rinit else [])
         for p, (y0, y1) in enumerate(parts):
             # epilogue stores per wave: two 16-byte pieces per row of its part (RowSink::row)
             npf = R - 2 * P if pers[mode] else 0
@@ -487,7 +491,10 @@ def gen_config(k, m):
             out.append(f"    uint32_t acc[{nr}][8];")
             # opaque zeros: a constant 0 would be folded into the first step, whose pinned results
             # then need register copies of shared table entries (AGPR spills at k=200).
-            out.append(f"    for (int y = 0; y < {nr}; ++y) for (int b = 0; b < 8; ++b) ZERO(acc[y][b]);")
+            if rinit:
+                out.extend(f"    src.rrow({y0 + yi}, acc[{yi}]);" for yi in range(nr))
+            else:
+                out.append(f"    for (int y = 0; y < {nr}; ++y) for (int b = 0; b < 8; ++b) ZERO(acc[y][b]);")
             out.append(body)
             out.append("    __builtin_amdgcn_sched_barrier(0);")
             out.append(f"    // epilogue: store rows {y0}..{y1 - 1}")
