@@ -58,7 +58,8 @@ int cauchy_256_batch_reserve_stream(int k, int m, int block_bytes, int groups, v
  * cauchy_256_decode_batch_out. Counts are kept per stream: this waits for `stream` and returns the
  * number of such groups among the decodes enqueued on `stream` since the previous call for that
  * stream (read and reset in stream order), or -2 on a GPU error. The single-group
- * cauchy_256_decode returns -1 for such a group (it decodes on cauchy_256_default_stream()).
+ * cauchy_256_decode returns -1 for such a group and counts it nowhere (it decodes on a private
+ * staging stream).
  * Every entry point runs on the library's device and restores the calling thread's current HIP
  * device before it returns. */
 int cauchy_256_batch_errors(void *stream);
@@ -82,8 +83,9 @@ int cauchy_256_erasure_pattern(unsigned long long g, int k, int m, unsigned long
  * inside one 4 GB page (checked at launch, generic kernels otherwise); afterwards it includes it. */
 int cauchy_256_batch_path(int k, int m, int block_bytes);
 
-/* The library's private stream (used by the single-group calls) and a synchronize helper for
- * callers without HIP. */
+/* The library's stream (the batched calls' stream when they are passed a null stream) and a
+ * synchronize helper for callers without HIP. The single-group calls use their own staging
+ * streams (up to 8, one per concurrent call), so calls from different threads overlap. */
 void *cauchy_256_default_stream(void);
 int cauchy_256_sync(void *stream);
 

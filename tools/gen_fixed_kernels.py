@@ -416,7 +416,12 @@ def shape(k, m):
     else:
         # Up to 16 waves per workgroup: the CW waves of one part run the SAME straight-line code in
         # lockstep (one barrier per step), so they share every instruction-cache line they fetch.
-        CW = int(os.environ.get("SH_CW", str(max(1, min(8, 8 // P)))))
+        # Two parts take CW = 2 and a 48 KB ring (R = 12, three 4-wave workgroups per CU): encode
+        # (64,16,1400) 0.122 vs 0.131 ms at 4,096 groups, (112,16,1400) 0.40 vs 0.46 ms, against
+        # CW = 4 with two 8-wave workgroups (round-4 A/B, profiles/r04/ab_runs.txt block 7).
+        CW = int(os.environ.get("SH_CW", str(2 if P == 2 else max(1, min(8, 8 // P)))))
+        if P == 2 and "SH_CW" not in os.environ and "SH_RING_BYTES" not in os.environ:
+            rbytes = 49152
     # LDS per workgroup: ring of R slots (the 2 KB per wave of store scratch aliases the ring after
     # the last step)
     slot = 8 * CW * 64 * 4
