@@ -239,11 +239,13 @@ struct WsLease {
     int *errors = nullptr;
 };
 
-int lease_workspace(Context &c, hipStream_t stream, size_t bytes, WsLease &out) {
+// reserve = false: the single-group calls' staging streams, sized by their own need only (up to
+// 8 of them; cauchy_256_batch_reserve is for the batched calls' streams).
+int lease_workspace(Context &c, hipStream_t stream, size_t bytes, WsLease &out, bool reserve = true) {
     StreamState *st = stream_state(c, stream);
     if (!st) return -2;
     out.lk = std::unique_lock<std::mutex>(st->mu);
-    if (st->ws.ensure(std::max(bytes, c.ws_reserve.load()), stream)) return -2;
+    if (st->ws.ensure(reserve ? std::max(bytes, c.ws_reserve.load()) : bytes, stream)) return -2;
     out.p = static_cast<uint8_t *>(st->ws.p);
     out.errors = st->d_errors;
     return 0;
@@ -749,7 +751,8 @@ int decode_batch(int k, int m, int B, int groups, uint8_t *d_blocks, uint8_t *d_
     if (k + m > 256 || B % 8 != 0) return invalid_decode_status(k, groups, d_rows, s);
     DecodeWS w{};
     WsLease ls;
-    if (int rc = lease_workspace(c, s, carve(w, nullptr, k, m, B, groups, true), ls)) return rc;
+    // slice_scratch: the single-group ABI (a staging stream, no batch reserve)
+    if (int rc = lease_workspace(c, s, carve(w, nullptr, k, m, B, groups, true), ls, slice_scratch == nullptr)) return rc;
     carve(w, ls.p, k, m, B, groups, true);
     if (int rc = decode_core(c, k, m, B, groups, d_blocks, d_rows, w, ls.errors, w.recovered, s, slice_scratch))
         return rc;

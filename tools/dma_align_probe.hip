@@ -12,6 +12,11 @@
 //   raw      3 whole groups per tile (132 columns): the 3 blocks as contiguous 1400-byte runs, read
 //            in 16-byte chunks aligned down to 16 (1408 bytes each)
 //   aligned  as gather with the sub-block size padded to 176 (what the lab's "algn" variant did)
+//   gorder   as gather, DMA lanes ordered (group, sub-block, chunk) instead of (sub-block, column)
+//   a16      as gather, each lane's offset rounded down to 16 (same lines, wrong bytes)
+//   xcd      as gather, tiles in XCD-aware order (neighbouring tiles share one L2)
+//   gord16   gorder with each lane's offset rounded down to 16 (contiguous and aligned, wrong bytes)
+//   gath3    gather over tiles of 3 whole groups (132 columns, the last 4 unread: timing only)
 // Every variant moves within 3 % of the same bytes; the time per byte is what differs.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -41,7 +46,14 @@ template <int MODE>
 __global__ __launch_bounds__(NT) void probe(const uint8_t *in, long long in_bytes, int groups, uint32_t *sink) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[R * 4096 + 256];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tile = blockIdx.x;
+    // MODE 5: gather with an XCD-aware order (workgroup i runs on XCD i % 8: consecutive tiles
+    // on one XCD, so a group split between two tiles is read through one L2)
+    int tile = blockIdx.x;
+    if (MODE == 5) {
+        const int per = (gridDim.x + 7) / 8, xcd = blockIdx.x % 8, i = blockIdx.x / 8;
+        tile = xcd * per + i;
+        if (tile >= (int)gridDim.x) return;  // (the few extra slots of the last XCD)
+    }
     uint32_t voff;
     long long base;
     if (MODE == 1) {
@@ -50,9 +62,32 @@ __global__ __launch_bounds__(NT) void probe(const uint8_t *in, long long in_byte
         const int i = threadIdx.x;                  // chunk 0..255 of 3 x 88 (the last 8 unread)
         const int r = i / 88, j = i - r * 88;
         voff = (g0 + r < groups) ? (uint32_t)(r * GSTRIDE + 16 * j) : 0x80000000u;
+    } else if (MODE == 3 || MODE == 6) {
+        // gorder: the product's 128-column tiles, DMA lanes ordered (group, sub-block, 4-column
+        // chunk) -- consecutive lanes walk a group's block nearly contiguously (the LDS image
+        // becomes [group segment][sub-block][columns], still 16-byte aligned per sub-block)
+        const long long col0 = (long long)tile * 128;
+        const int gf = (int)(col0 / NQ);
+        base = (long long)gf * GSTRIDE;
+        int i = threadIdx.x;  // chunk index 0..255
+        voff = 0x80000000u;
+        for (int g = gf; g * (long long)NQ < col0 + 128; ++g) {
+            const long long lo = g * (long long)NQ > col0 ? g * (long long)NQ : col0;
+            const long long hi = (g + 1) * (long long)NQ < col0 + 128 ? (g + 1) * (long long)NQ : col0 + 128;
+            const int nch = (int)((hi - lo) / 4), q0 = (int)(lo - g * (long long)NQ);
+            if (i < 8 * nch) {
+                const int a = i / nch, q = q0 + 4 * (i - a * nch);
+                const int co = 4 * q - (q >= NQ - 4 ? 4 * NQ - 175 : 0);
+                if (g < groups) voff = (uint32_t)((g - gf) * GSTRIDE + a * 175 + co);
+                if (MODE == 6 && voff != 0x80000000u) voff &= ~15u;  // contiguous AND aligned
+                break;
+            }
+            i -= 8 * nch;
+        }
     } else {
         const int sub = MODE == 2 ? 176 : 175;
-        const long long col0 = (long long)tile * 128;
+        // MODE 7: tiles of 3 whole groups (132 columns; the 128 lanes leave the last 4 unread)
+        const long long col0 = MODE == 7 ? (long long)tile * 132 : (long long)tile * 128;
         const int gf = (int)(col0 / NQ);
         base = (long long)gf * GSTRIDE;
         const int off = wave * 1024 + lane * W;
@@ -61,6 +96,7 @@ __global__ __launch_bounds__(NT) void probe(const uint8_t *in, long long in_byte
         const int g = (int)(colx / NQ), q = (int)(colx - (long long)g * NQ);
         const int co = 4 * q - (q >= NQ - 4 ? 4 * NQ - sub : 0);
         voff = (g < groups) ? (uint32_t)((g - gf) * GSTRIDE + a * sub + co) : 0x80000000u;
+        if (MODE == 4 && voff != 0x80000000u) voff &= ~15u;  // (MODE 5: as 0)  // same lines, 16-byte aligned lanes
     }
     const __amdgpu_buffer_rsrc_t rs = rsrc_of(in + base, in_bytes - base);
     uint8_t *slot0 = ring + wave * 1024;
@@ -94,22 +130,27 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     const int tiles_g = (int)((groups * (long long)NQ + 127) / 128), tiles_r = (groups + 2) / 3;
-    const char *names[3] = {"gather", "raw", "aligned"};
+    const char *names[8] = {"gather", "raw", "aligned", "gorder", "a16", "xcd", "gord16", "gath3"};
     for (int rep = 0; rep < 2; ++rep)
-        for (int mode = 0; mode < 3; ++mode) {
+        for (int mode = 0; mode < 8; ++mode) {
             float best = 1e9f;
             for (int it = 0; it < 10; ++it) {
                 CK(hipEventRecord(e0));
                 if (mode == 0) hipLaunchKernelGGL(probe<0>, dim3(tiles_g), dim3(NT), 0, 0, in, bytes, groups, sink);
                 if (mode == 1) hipLaunchKernelGGL(probe<1>, dim3(tiles_r), dim3(NT), 0, 0, in, bytes, groups, sink);
                 if (mode == 2) hipLaunchKernelGGL(probe<2>, dim3(tiles_g), dim3(NT), 0, 0, in, bytes, groups, sink);
+                if (mode == 3) hipLaunchKernelGGL(probe<3>, dim3(tiles_g), dim3(NT), 0, 0, in, bytes, groups, sink);
+                if (mode == 4) hipLaunchKernelGGL(probe<4>, dim3(tiles_g), dim3(NT), 0, 0, in, bytes, groups, sink);
+                if (mode == 5) hipLaunchKernelGGL(probe<5>, dim3(tiles_g), dim3(NT), 0, 0, in, bytes, groups, sink);
+                if (mode == 6) hipLaunchKernelGGL(probe<6>, dim3(tiles_g), dim3(NT), 0, 0, in, bytes, groups, sink);
+                if (mode == 7) hipLaunchKernelGGL(probe<7>, dim3(tiles_r), dim3(NT), 0, 0, in, bytes, groups, sink);
                 CK(hipEventRecord(e1));
                 CK(hipEventSynchronize(e1));
                 float ms;
                 CK(hipEventElapsedTime(&ms, e0, e1));
                 if (ms < best) best = ms;
             }
-            const double moved = (double)(mode == 1 ? tiles_r : tiles_g) * K * 4096.0;  // DMA'd bytes
+            const double moved = (double)(mode == 1 || mode == 7 ? tiles_r : tiles_g) * K * 4096.0;  // DMA'd bytes
             printf("%-8s groups %d  best %.4f ms  %.0f GB/s DMA'd  %.0f GB/s of block bytes\n", names[mode], groups,
                    best, moved / best / 1e6, (double)groups * K * B / best / 1e6);
         }
