@@ -214,10 +214,11 @@ struct Src {
         lbase = w.valid ? static_cast<uint32_t>(w.gl) * static_cast<uint32_t>(a.in_gstride) + col_off(w.q, geo) : OOR;
     }
 
-    // Decode: residual row y starts as the received recovery block R_y (position entry KP + y;
-    // absent: zeros), loaded straight into the lane's 8 accumulators before the ring's first
-    // DMA, so stage A runs the k input steps only (no m extra ring steps). Older than every DMA,
-    // these loads are covered by the ring's counted waits; the compiler's own wait guards the use.
+    // Decode, generator switch SH_RINIT=1 (not the default: same time, more fetched bytes):
+    // residual row y starts as the received recovery block R_y (position entry KP + y; absent:
+    // zeros), loaded straight into the lane's 8 accumulators before the ring's first DMA, so
+    // stage A runs the k input steps only. Older than every DMA, these loads are covered by the
+    // ring's counted waits; the compiler's own wait guards the use.
     __device__ __forceinline__ void rrow(int y, uint32_t (&r)[8]) const {
         const int p = pos[lgl * (S::KP + S::MP) + S::KP + y];
         const uint32_t o = (p == 0xFF || lbase == OOR) ? OOR : lbase + static_cast<uint32_t>(p) * B;

@@ -17,7 +17,7 @@ spills even at k=28).
 One generated kernel serves two modes (template flag DEC):
   encode       recovery[g][y] = sum_x M(C[y][x]) data[g][x]             (y < m, row 0 = ones)
   decode A     residual[g][y] = R_y + sum_{x received} M(C[y][x]) d_x   (erased x read as zeros;
-               R_y loaded into the accumulators before the k input steps)
+               R_y streamed through the same ring as m extra steps after the k input steps)
 Rows are split into parts of <= 9 rows (<= 72 accumulator VGPRs); the waves of one workgroup
 run the parts of the same columns and read the same LDS ring slots.
 
@@ -437,9 +437,11 @@ def shape(k, m):
 
 
 PERSIST = os.environ.get("SH_PERSIST", "0") == "1"
-# Decode stage A: residual rows start as the recovery blocks R_y, loaded into the accumulators in
-# the prologue (Src::rrow), instead of m extra ring steps (0: the ring steps, A/B only).
-RINIT = os.environ.get("SH_RINIT", "1") == "1"
+# Decode stage A, SH_RINIT=1 (measured, not the default): residual rows start as the recovery
+# blocks R_y, loaded into the accumulators in the prologue (Src::rrow) instead of m extra ring
+# steps -- same time (ab_runs.txt block 7), but the per-lane dword loads fetch those rows at
+# ~1.6x their bytes (stage A reads 2.63 vs 2.42 GB per launch).
+RINIT = os.environ.get("SH_RINIT", "0") == "1"
 
 
 PERSIST_DEC = os.environ.get("SH_PERSIST_DEC", "1") == "1"
