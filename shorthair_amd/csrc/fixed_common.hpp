@@ -74,6 +74,7 @@ namespace fixed {
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32_ua __attribute__((aligned(1)));  // byte-aligned dword (LDS reads it unaligned)
 constexpr uint32_t OOR = 0x80000000u;  // buffer offset past every descriptor's range (< 2 GiB)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const uint8_t *p, uint32_t bytes) {
@@ -337,6 +338,29 @@ struct Src {
         return r;
     }
 
+    // The position entries of up to 4 consecutive steps t..t+3 in one (byte-unaligned) LDS read,
+    // taken one burst of DMA issues ahead: the issues of a burst then never wait on LDS (one
+    // ds_read_u8 per step, each consumed by the next issue, put an LDS latency between every two
+    // DMAs of a burst). The table has 4 bytes of padding past its last group.
+    struct Pre4 {
+        uint32_t w[S::DPW];
+    };
+    __device__ __forceinline__ Pre4 pre4(int t) const {
+        Pre4 r;
+#pragma unroll
+        for (int j = 0; j < S::DPW; ++j) {
+            r.w[j] = 0;
+            if (DEC) r.w[j] = *reinterpret_cast<const u32_ua *>(pos + dgl[j] * (S::KP + S::MP) + t);
+        }
+        return r;
+    }
+    __device__ __forceinline__ void issue4(int x, const Pre4 &p4, int i) const {
+        Pre r;
+#pragma unroll
+        for (int j = 0; j < S::DPW; ++j) r.p[j] = static_cast<int>((p4.w[j] >> (8 * i)) & 0xFFu);
+        issue(x, r);
+    }
+
     // DMA of step x into its ring slot (encode: input block x).
     __device__ __forceinline__ void issue(int x, const Pre &pr) const {
         uint8_t *slot = const_cast<uint8_t *>(lds) + (x % S::R) * S::SLOT;
@@ -415,6 +439,19 @@ struct StreamSrc {
         Pre r;
         r.p = DEC ? pos[gl * (S::KP + S::MP) + t] : 0;
         return r;
+    }
+    struct Pre4 {
+        uint32_t w;
+    };
+    __device__ __forceinline__ Pre4 pre4(int t) const {  // as Src::pre4
+        Pre4 r{0};
+        if (DEC) r.w = *reinterpret_cast<const u32_ua *>(pos + gl * (S::KP + S::MP) + t);
+        return r;
+    }
+    __device__ __forceinline__ void issue4(int x, const Pre4 &p4, int i) const {
+        Pre r;
+        r.p = static_cast<int>((p4.w >> (8 * i)) & 0xFFu);
+        issue(x, r);
     }
     __device__ __forceinline__ void issue(int x, const Pre &pr) const {
         uint32_t o = lane_base, so = 0;
@@ -632,7 +669,8 @@ inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArg
     // ring (the row images of the epilogue alias it); a streaming source needs only the images
     constexpr size_t front = STREAM ? 2ull * S::P * S::SLOT : static_cast<size_t>(S::R) * S::SLOT;
     static_assert(STREAM || 2 * S::P <= S::R, "row images must fit inside the ring");
-    const size_t lds = front + (dec ? static_cast<size_t>(a.groups_per_wg) * (S::KP + S::MP) : 0);
+    // (+4: Src::pre4 reads up to 3 bytes past the last group's table)
+    const size_t lds = front + (dec ? static_cast<size_t>(a.groups_per_wg) * (S::KP + S::MP) + 4 : 0);
     const long long cols = static_cast<long long>(a.groups) * a.geo.nq;
     unsigned blocks = static_cast<unsigned>((cols + S::COLS - 1) / S::COLS);  // one tile each
     if (PERS) blocks = std::min<unsigned>(blocks, static_cast<unsigned>(persistent_slots()));

@@ -186,6 +186,12 @@ class Body:
         def wait(T, I):
             ex = st if T < npf else 0
             return f"    src.template wait<{T}, {I}, {ex}>();" if ex else f"    src.template wait<{T}, {I}>();"
+
+        def consec(a, b):  # steps a..b-1 have consecutive position-table entries
+            return all(tidx(steps[a + i]) == tidx(steps[a]) + i for i in range(b - a))
+        # Position entries are read 4 steps per LDS read, one burst of issues ahead (Src::pre4);
+        # the persistent form (npf > 0) keeps one read per step.
+        P4 = npf == 0
         if dma:
             if npf:
                 L.append("    if (!src.pref) {")
@@ -195,15 +201,29 @@ class Body:
                 L.append("    } else {")
                 L.append("    src.images_done();")
                 L.append("    }")
-            for t in range(npf, nxt_issue):
-                L.append(f"    src.issue({t}, src.pre({tidx(steps[t])}));")
+            if P4:
+                chunks = [(c, min(c + 4, nxt_issue)) for c in range(0, nxt_issue, 4)]
+                for c0, c1 in chunks:
+                    if consec(c0, c1):
+                        L.append(f"    const typename Src::Pre4 q{c0} = src.pre4({tidx(steps[c0])});")
+                for c0, c1 in chunks:
+                    for t in range(c0, c1):
+                        L.append(f"    src.issue4({t}, q{c0}, {t - c0});" if consec(c0, c1)
+                                 else f"    src.issue({t}, src.pre({tidx(steps[t])}));")
+            else:
+                for t in range(npf, nxt_issue):
+                    L.append(f"    src.issue({t}, src.pre({tidx(steps[t])}));")
         need = units[1][-1] if len(units) > 1 else units[0][-1]
         landed = min(n - 1, max(need, S - 1), nxt_issue - 1)
         assert need <= landed
         L.append(wait(landed, nxt_issue))
         read_unit(0, "dA")
         if nxt_issue < n:
-            L.append(f"    typename Src::Pre pre = src.pre({tidx(steps[nxt_issue])});")
+            if P4:
+                L.append(f"    typename Src::Pre4 pre4 = src.pre4({tidx(steps[nxt_issue])});")
+            else:
+                L.append(f"    typename Src::Pre pre = src.pre({tidx(steps[nxt_issue])});")
+        b4 = nxt_issue  # first step covered by pre4
         for u, unit in enumerate(units):
             cur, nxt = ("dA", "dB") if u % 2 == 0 else ("dB", "dA")
             L.append("    // ---- " + ", ".join(f"step {t}: " + (f"input block {steps[t][1]}" if steps[t][0] == "c"
@@ -219,12 +239,23 @@ class Body:
                     assert nu[-1] <= landed, "ring too small for the unit size"
                     if "nobar" not in ABLATE:
                         L.append(wait(landed, nxt_issue))
+                    issued = False
                     while nxt_issue < n and nxt_issue - R <= unit[0] - 1:
-                        if dma:
+                        if dma and P4:
+                            x = nxt_issue
+                            if x - b4 < 4 and consec(b4, x + 1):
+                                L.append(f"    src.issue4({x}, pre4, {x - b4});")
+                            else:
+                                L.append(f"    src.issue({x}, src.pre({tidx(steps[x])}));")
+                        elif dma:
                             L.append(f"    src.issue({nxt_issue}, pre);")
                         nxt_issue += 1
-                        if nxt_issue < n:
+                        issued = True
+                        if nxt_issue < n and not P4:
                             L.append(f"    pre = src.pre({tidx(steps[nxt_issue])});")
+                    if P4 and issued and nxt_issue < n:
+                        L.append(f"    pre4 = src.pre4({tidx(steps[nxt_issue])});")
+                        b4 = nxt_issue
                 if not READ_LATE:
                     read_unit(u + 1, nxt)
                 if READ_PIN:
