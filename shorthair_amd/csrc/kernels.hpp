@@ -123,6 +123,7 @@ struct StageBV2Args {
     int groups;
     Geometry geo;
     uint64_t snip_base;       // address of snippet 0 of the accumulating table (stride SNIP_STRIDE)
+    int j_base;               // set by the launcher: first output of the launch (a tail launch)
 };
 bool stageb_v2_ok(const Geometry &geo, int emax);
 hipError_t launch_stageb_v2(const StageBV2Args &a, hipStream_t stream);

@@ -541,10 +541,11 @@ constexpr int V2_MAXE = 128;  // emax = min(k, m) <= 128 whenever k + m <= 256
 
 // Ring depth: 16 rows (4 per barrier group) for 4- and 8-wave workgroups; 8 rows (2 per group)
 // for the 1- and 2-wave workgroups of emax <= 16, so their 16 KB rings let 9 of them share a CU.
-template <int NW>
+// MAXE: the rows a wave's coefficient copy holds (16 for the 1-2-wave workgroups of emax <= 16;
+// V2_MAXE for the others, and for the 1-2-wave tail launches of a larger emax).
+template <int NW, int MAXE = (NW <= 2 ? 16 : V2_MAXE)>
 __global__ __launch_bounds__(64 * NW) void stageb_v2(StageBV2Args a) {
     constexpr int RB_R = NW <= 2 ? 8 : 16, RB_S = RB_R / 4;
-    constexpr int MAXE = NW <= 2 ? 16 : V2_MAXE;  // 1-2 waves: emax <= 16 (launch_stageb_v2)
     __shared__ __attribute__((aligned(16))) uint8_t ring[RB_R * RB_ROW];
     __shared__ __attribute__((aligned(8))) uint32_t cf[NW][MAXE][2];  // [wave][row] coefficient bytes
     const Geometry geo = a.geo;
@@ -555,7 +556,7 @@ __global__ __launch_bounds__(64 * NW) void stageb_v2(StageBV2Args a) {
     const int ncols = min(64, geo.nq - c0);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int j0 = (blockIdx.y * NW + wave) * 8;
+    const int j0 = a.j_base + (blockIdx.y * NW + wave) * 8;
     // The prologue's loads do not depend on e (a scalar load of its own): the row list and this
     // wave's coefficient bytes are loaded for emax rows at once (entries past e are in the
     // group's workspace, unused), so e, the rows and the coefficients take one memory latency
@@ -679,16 +680,33 @@ hipError_t launch_stageb_v2(const StageBV2Args &a, hipStream_t stream) {
     const int nw = (force == 1 || force == 2) && octets <= 2 ? force                       // 1-2 waves hold <= 16 rows
                    : (force == 4 || force == 8) ? force
                    : (octets <= 2 ? octets : (8 * c8 <= 4 * c4 ? 8 : 4));
-    const int chunks = (octets + nw - 1) / nw;
+    // A last chunk with fewer octets than waves (e = 66: 3 x 4 waves, the third with one active
+    // wave) runs as its own launch of 1- or 2-wave workgroups instead: no idle waves holding
+    // registers and barrier slots (SH_V2_NO_TAIL: measurement switch).
+    static const bool no_tail = std::getenv("SH_V2_NO_TAIL") != nullptr;
+    int chunks = (octets + nw - 1) / nw;
+    const int rem = octets - (chunks - 1) * nw;  // octets of the last chunk
+    const bool tail = !no_tail && chunks > 1 && rem <= 2 && nw >= 4;
+    if (tail) --chunks;
+    StageBV2Args m = a;
+    m.j_base = 0;
     dim3 grid(static_cast<unsigned>(ncc) * a.groups, chunks, 1);
     if (nw == 1)
-        hipLaunchKernelGGL(stageb_v2<1>, grid, dim3(64), 0, stream, a);
+        hipLaunchKernelGGL(stageb_v2<1>, grid, dim3(64), 0, stream, m);
     else if (nw == 2)
-        hipLaunchKernelGGL(stageb_v2<2>, grid, dim3(128), 0, stream, a);
+        hipLaunchKernelGGL(stageb_v2<2>, grid, dim3(128), 0, stream, m);
     else if (nw == 4)
-        hipLaunchKernelGGL(stageb_v2<4>, grid, dim3(256), 0, stream, a);
+        hipLaunchKernelGGL(stageb_v2<4>, grid, dim3(256), 0, stream, m);
     else
-        hipLaunchKernelGGL(stageb_v2<8>, grid, dim3(512), 0, stream, a);
+        hipLaunchKernelGGL(stageb_v2<8>, grid, dim3(512), 0, stream, m);
+    if (tail) {
+        m.j_base = chunks * nw * 8;
+        dim3 tg(static_cast<unsigned>(ncc) * a.groups, 1, 1);
+        if (rem == 1)
+            hipLaunchKernelGGL((stageb_v2<1, V2_MAXE>), tg, dim3(64), 0, stream, m);
+        else
+            hipLaunchKernelGGL((stageb_v2<2, V2_MAXE>), tg, dim3(128), 0, stream, m);
+    }
     return hipGetLastError();
 }
 
