@@ -684,23 +684,25 @@ hipError_t launch_stageb_v2(const StageBV2Args &a, hipStream_t stream) {
     // wave) runs as its own launch of 1- or 2-wave workgroups instead: no idle waves holding
     // registers and barrier slots (SH_V2_NO_TAIL: measurement switch).
     static const bool no_tail = std::getenv("SH_V2_NO_TAIL") != nullptr;
-    int chunks = (octets + nw - 1) / nw;
-    const int rem = octets - (chunks - 1) * nw;  // octets of the last chunk
-    const bool tail = !no_tail && chunks > 1 && rem <= 2 && nw >= 4;
+    // One 8-wave chunk with 5 or 6 octets (e = 33..48): a 4-wave chunk plus a 1-2-wave tail.
+    const int nw1 = (!no_tail && force == 0 && nw == 8 && (octets == 5 || octets == 6)) ? 4 : nw;
+    int chunks = (octets + nw1 - 1) / nw1;
+    const int rem = octets - (chunks - 1) * nw1;  // octets of the last chunk
+    const bool tail = !no_tail && chunks > 1 && rem <= 2 && nw1 >= 4;
     if (tail) --chunks;
     StageBV2Args m = a;
     m.j_base = 0;
     dim3 grid(static_cast<unsigned>(ncc) * a.groups, chunks, 1);
-    if (nw == 1)
+    if (nw1 == 1)
         hipLaunchKernelGGL(stageb_v2<1>, grid, dim3(64), 0, stream, m);
-    else if (nw == 2)
+    else if (nw1 == 2)
         hipLaunchKernelGGL(stageb_v2<2>, grid, dim3(128), 0, stream, m);
-    else if (nw == 4)
+    else if (nw1 == 4)
         hipLaunchKernelGGL(stageb_v2<4>, grid, dim3(256), 0, stream, m);
     else
         hipLaunchKernelGGL(stageb_v2<8>, grid, dim3(512), 0, stream, m);
     if (tail) {
-        m.j_base = chunks * nw * 8;
+        m.j_base = chunks * nw1 * 8;
         dim3 tg(static_cast<unsigned>(ncc) * a.groups, 1, 1);
         if (rem == 1)
             hipLaunchKernelGGL((stageb_v2<1, V2_MAXE>), tg, dim3(64), 0, stream, m);
