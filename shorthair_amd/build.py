@@ -92,6 +92,7 @@ def build(force=False, verbose=True, jobs=None):
     straight-line function, ~1-2 min for k=200) and link libcauchy256.so."""
     gen_script = os.path.join(HERE, "..", "tools", "gen_fixed_kernels.py")
     gen_inputs = max(os.path.getmtime(gen_script),
+                     os.path.getmtime(os.path.join(HERE, "..", "tools", "xor_sched.py")),
                      os.path.getmtime(os.path.join(CSRC, "cauchy_tables_data.h")))
     if (force or not os.path.isdir(GEN_DIR) or not _gen_sources()
             or min(os.path.getmtime(f) for f in _gen_sources()) < gen_inputs):

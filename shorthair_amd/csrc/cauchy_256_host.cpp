@@ -89,6 +89,10 @@ struct StreamState {
     std::mutex mu;
     DevBuf ws;
     int *d_errors = nullptr;
+    // chunk-pipelined decode (decode_core): stage B of chunk j on `side` beside stage A of chunk
+    // j + 1 on the calling stream, joined by `evs` (created on first use, guarded by mu)
+    hipStream_t side = nullptr;
+    std::vector<hipEvent_t> evs;
 };
 
 // One launch of the tile kernels: output rows [row0, row0 + nrows) with its snippet-address table.
@@ -634,6 +638,12 @@ hipError_t launch_stage_b(const DecodeWS &w, int n_in, int B, int groups, uint8_
     return sh::launch_stageb(b, w.emax, s);
 }
 
+// Chunks of the pipelined decode (SH_DEC_CHUNKS, measurement switch; 1 = one launch per stage)
+int dec_chunks(int groups) {
+    static const int n = std::getenv("SH_DEC_CHUNKS") ? std::atoi(std::getenv("SH_DEC_CHUNKS")) : 1;
+    return (n > 1 && groups >= 256 * n) ? n : 1;
+}
+
 // Common decode core (m >= 2, valid params): writes recovered blocks densely into `dst`
 // ([G][emax][B]) and leaves per-group e / rec_idx / erasures in the workspace.
 int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_blocks,
@@ -682,6 +692,42 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
     if (ev) SH_CHECK(hipEventRecord(ev[1], s));
 
     const Geometry geo = sh::make_geometry(B);
+    const int nch = dec_chunks(groups);
+    if (w.fixed && w.v2 && nch > 1 && !slice_scratch && sh::has_fixed(k, m, B) && !force_tile()) {
+        // Chunk-pipelined (measurement switch SH_DEC_CHUNKS): stage A of chunk j on `s`, stage B
+        // of chunk j on a side stream once that stage A is done, so stage B (snippet calls: SALU
+        // and latency) runs beside the next chunk's stage A (VALU and memory).
+        StreamState *ss = stream_state(c, s);
+        if (!ss) return -2;
+        if (!ss->side) SH_CHECK(hipStreamCreateWithFlags(&ss->side, hipStreamNonBlocking));
+        while (static_cast<int>(ss->evs.size()) < nch + 1) {
+            hipEvent_t e;
+            SH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            ss->evs.push_back(e);
+        }
+        for (int j = 0; j < nch; ++j) {
+            const int lo = static_cast<int>(static_cast<long long>(groups) * j / nch);
+            const int n = static_cast<int>(static_cast<long long>(groups) * (j + 1) / nch) - lo;
+            SH_CHECK(launch_fixed_batch(k, m, B, n, d_blocks + static_cast<size_t>(lo) * k * B,
+                                        static_cast<long long>(k) * B,
+                                        w.residual + static_cast<size_t>(lo) * m * B, static_cast<long long>(m) * B,
+                                        w.pos + static_cast<size_t>(lo) * round4(k),
+                                        w.rpos + static_cast<size_t>(lo) * round4(m), true, s));
+            SH_CHECK(hipEventRecord(ss->evs[j], s));
+            SH_CHECK(hipStreamWaitEvent(ss->side, ss->evs[j], 0));
+            DecodeWS v = w;
+            v.e += lo;
+            v.rrow += static_cast<size_t>(lo) * round4(w.emax);
+            v.coefB += static_cast<size_t>(lo) * w.coefB_gs;
+            v.residual += static_cast<size_t>(lo) * m * B;
+            SH_CHECK(launch_stage_b(v, m, B, n, dst + static_cast<size_t>(lo) * w.emax * B, ss->side));
+        }
+        if (ev) SH_CHECK(hipEventRecord(ev[2], s));
+        SH_CHECK(hipEventRecord(ss->evs[nch], ss->side));
+        SH_CHECK(hipStreamWaitEvent(s, ss->evs[nch], 0));
+        if (ev) SH_CHECK(hipEventRecord(ev[3], s));
+        return 0;
+    }
     if (w.fixed) {
         // Stage A (compile-time generator, all m rows, erased columns read as zeros):
         //   residual_y = R_y + sum_{received x} M(C[y][x]) d_x
@@ -1108,7 +1154,38 @@ extern "C" int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes) {
     SH_CHECK(hipMemcpyAsync(d, h, data_bytes + k, hipMemcpyHostToDevice, st.stream));
     const int rc = decode_batch(k, m, block_bytes, 1, d, d + data_bytes, st.stream, e_host, d + data_bytes + 256);
     if (rc != 0) return rc;
-    SH_CHECK(hipMemcpyAsync(h, d, data_bytes + k, hipMemcpyDeviceToHost, st.stream));
+    // Download only what the codec may change: the row bytes and the blocks at positions whose
+    // row was >= k (the whole group went back, 280 KB at k = 200, B = 1400). One
+    // copy per contiguous run of such positions; past 4 runs, one copy over their whole span.
+    SH_CHECK(hipMemcpyAsync(h + data_bytes, d + data_bytes, k, hipMemcpyDeviceToHost, st.stream));
+    {
+        int runs[4][2], nr = 0, first = -1, last = -1;
+        bool many = false;
+        for (int i = 0; i < k; ++i) {
+            if (blocks[i].row < k) continue;
+            if (first < 0) first = i;
+            if (nr > 0 && runs[nr - 1][1] == i) {
+                runs[nr - 1][1] = i + 1;
+            } else if (nr < 4) {
+                runs[nr][0] = i;
+                runs[nr][1] = i + 1;
+                ++nr;
+            } else {
+                many = true;
+            }
+            last = i;
+        }
+        if (many) {
+            nr = 1;
+            runs[0][0] = first;
+            runs[0][1] = last + 1;
+        }
+        for (int r = 0; r < nr; ++r) {
+            const size_t o = static_cast<size_t>(runs[r][0]) * block_bytes;
+            SH_CHECK(hipMemcpyAsync(h + o, d + o, static_cast<size_t>(runs[r][1] - runs[r][0]) * block_bytes,
+                                    hipMemcpyDeviceToHost, st.stream));
+        }
+    }
     SH_CHECK(hipStreamSynchronize(st.stream));
     const int e = *e_host;
     // A group with more recovery blocks than erasures (outside the reference's contract: its

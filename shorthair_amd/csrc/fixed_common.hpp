@@ -103,7 +103,8 @@ struct Shape {
     static constexpr bool DMA = DMA_;
     static constexpr int NW = CW * P, NT = 64 * NW, COLS = CW * 64;
     static constexpr int ROWB = COLS * 4;               // bytes of one sub-block row of a slot
-    static constexpr int SLOT = 8 * ROWB;               // bytes per ring slot (one input block)
+    static constexpr int IMG = 8 * ROWB;                // bytes of one epilogue row image
+    static constexpr int SLOT = IMG;                    // bytes per ring slot (one input block)
     static constexpr int NDMA = SLOT / (64 * W);        // DMA wave-instructions per step
     static constexpr int DPW = (NDMA + NW - 1) / NW;    // ... issued by each wave (at most)
     static constexpr int KP = (K + 3) & ~3, MP = (M + 3) & ~3;
@@ -508,7 +509,7 @@ struct RowSink {
                                          int img_slot = 0) {
         rsrc = wg_rsrc(a.out, a.out_bytes, a.out_gstride, w.g_first);
         B = a.geo.B;
-        img = lds + (img_slot + part) * S::SLOT;
+        img = lds + img_slot * S::SLOT + part * S::IMG;
         col0 = w.col0;
         lo = w.lo;
         hi = w.hi;
@@ -529,29 +530,47 @@ struct RowSink {
         geo.sub = sub;
         geo.nq = nq;
         geo.tail = 4;
+        // Groups overlapping the tile: the first (from column cs) and the last may be partial, every
+        // one between is whole (8 * nq / 4 = 2 * nq pieces). O(1) per piece: the round-4 walk over
+        // the tile's groups cost up to 64 iterations of 64-bit arithmetic per piece at nq = 8
+        // (B = 256: a 512-column tile spans 64 groups), a regression of (28,4,256).
+        const long long g0 = cs / nq;
+        const int qa0 = static_cast<int>(cs - g0 * nq);
+        const int n0 = static_cast<int>(((ce < (g0 + 1) * nq ? ce : (g0 + 1) * nq) - cs) >> 2);  // chunks
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             int rem = (cw * 2 + h) * 64 + lane;  // piece index in memory order
             gdst[h] = OOR;
             lsrc[h] = 0;
-            for (long long g = cs / nq; g * nq < ce; ++g) {  // groups overlapping the tile
-                const int qa = static_cast<int>((cs > g * nq ? cs : g * nq) - g * nq);
-                const int qb = static_cast<int>((ce < (g + 1) * nq ? ce : (g + 1) * nq) - g * nq);
-                const int nch = (qb - qa) >> 2;  // whole chunks: tile and group edges are multiples of 4
-                if (rem < 8 * nch) {
-                    const int b = rem / nch, q = qa + 4 * (rem - b * nch);
-                    gdst[h] = static_cast<uint32_t>(g - g_first) * out_gstride +
-                              col_off(q, geo) + static_cast<uint32_t>(b * geo.sub);
-                    lsrc[h] = static_cast<uint32_t>(b * S::ROWB) + static_cast<uint32_t>(g * nq + q - col0) * 4u;
-                    break;
-                }
-                rem -= 8 * nch;
+            long long g;
+            int b, q;
+            bool ok;
+            if (rem < 8 * n0) {
+                g = g0;
+                b = rem / n0;
+                q = qa0 + 4 * (rem - b * n0);
+                ok = true;
+            } else {
+                rem -= 8 * n0;
+                const int gi = rem / (2 * nq);
+                g = g0 + 1 + gi;
+                rem -= gi * 2 * nq;
+                const long long gend = (ce < (g + 1) * nq ? ce : (g + 1) * nq);
+                const int ng = g * nq < ce ? static_cast<int>((gend - g * nq) >> 2) : 0;
+                ok = rem < 8 * ng;
+                b = ok ? rem / ng : 0;
+                q = ok ? 4 * (rem - b * ng) : 0;
+            }
+            if (ok) {
+                gdst[h] = static_cast<uint32_t>(g - g_first) * out_gstride +
+                          col_off(q, geo) + static_cast<uint32_t>(b * geo.sub);
+                lsrc[h] = static_cast<uint32_t>(b * S::ROWB) + static_cast<uint32_t>(g * nq + q - col0) * 4u;
             }
         }
     }
     template <int YI>
     __device__ __forceinline__ void row(int y, const uint32_t (&w)[8]) const {
-        uint8_t *im = img + (YI & 1) * S::P * S::SLOT;
+        uint8_t *im = img + (YI & 1) * S::P * S::IMG;
 #pragma unroll
         for (int b = 0; b < 8; ++b) *reinterpret_cast<uint32_t *>(im + b * S::ROWB + wofs) = w[b];
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -571,9 +590,9 @@ struct RowSink {
 // lanes) and returns this wave's part. The caller (the FIXED_KERNEL macro)
 // then calls the generated run_<name> directly, so everything inlines into one function: a
 // non-inlined body took `src` by reference through scratch and read the LDS ring with flat loads.
-template <class S, bool DEC, class SrcT>
+template <class S, bool DEC, class SrcT, class SinkT>
 __device__ __forceinline__ int kernel_prologue(const FixedArgs &a, uint8_t *lds, SrcT &src,
-                                               RowSink<S> &sink, long long col0, long long lo, long long hi,
+                                               SinkT &sink, long long col0, long long lo, long long hi,
                                                int img_slot = 0) {
     const WGInfo w = tile_info<S>(a.geo.nq, col0, lo, hi);
     const int part = w.wave % S::P;
@@ -668,7 +687,7 @@ inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArg
     a.groups_per_wg = (S::COLS - 1) / a.geo.nq + 2;
     // ring (the row images of the epilogue alias it); a streaming source needs only the images
     constexpr size_t front = STREAM ? 2ull * S::P * S::SLOT : static_cast<size_t>(S::R) * S::SLOT;
-    static_assert(STREAM || 2 * S::P <= S::R, "row images must fit inside the ring");
+    static_assert(STREAM || 2 * S::P * S::IMG <= S::R * S::SLOT, "row images must fit inside the ring");
     // (+4: Src::pre4 reads up to 3 bytes past the last group's table)
     const size_t lds = front + (dec ? static_cast<size_t>(a.groups_per_wg) * (S::KP + S::MP) + 4 : 0);
     const long long cols = static_cast<long long>(a.groups) * a.geo.nq;

@@ -576,7 +576,9 @@ __global__ __launch_bounds__(64 * NW) void stageb_v2(StageBV2Args a) {
         __builtin_memcpy(&cfw[u], cg + static_cast<long long>(i >> 1) * a.ldT + 4 * (i & 1), 4);
     }
     const int e = a.e[g];
-    if (e <= 0) return;  // uniform over the workgroup
+    // uniform over the workgroup: no erasures, or no output of this chunk below e (a group with
+    // fewer erasures than emax: its later chunks would stream every row for nothing)
+    if (e <= 0 || a.j_base + static_cast<int>(blockIdx.y) * NW * 8 >= e) return;
     const bool active = j0 < e;
     const long long gbase = static_cast<long long>(g) * a.in_gstride;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(

@@ -42,7 +42,7 @@ template <int P_, int CW_>
 struct TShape {
     static constexpr int P = P_, CW = CW_, W = 16;
     static constexpr int NW = CW * P, NT = 64 * NW, COLS = CW * 64;
-    static constexpr int ROWB = COLS * 4, SLOT = 8 * ROWB;
+    static constexpr int ROWB = COLS * 4, SLOT = 8 * ROWB, IMG = SLOT;
     static constexpr int NDMA = SLOT / (64 * W);
     static constexpr int DPW = (NDMA + NW - 1) / NW;
     // ring: <= 64 KB (two workgroups per CU; ds_read offsets), at least 2P slots (the row images alias it)

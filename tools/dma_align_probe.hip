@@ -118,6 +118,142 @@ __global__ __launch_bounds__(NT) void probe(const uint8_t *in, long long in_byte
     if (acc == 0x12345678u) sink[threadIdx.x] = acc;
 }
 
+
+// MODE blk (round 5): the product's 128-column tiles in XCD-aware order, but each step reads the
+// WHOLE block of every group the tile touches (3-4 groups) as one contiguous 16-byte-aligned run of
+// 88 chunks (1408 bytes; odd blocks start 8 bytes early): a lane would then read its words with
+// unaligned ds_read_b32 from the raw block image. Edge groups are read by both neighbouring tiles
+// (same XCD, same time: the second read hits L2). RB slots of 6 KB, SB steps per barrier, 2 DMA
+// issues per wave and step (the 6th..8th 1 KB pieces only where the tile touches groups).
+template <int RB, int SB, bool XCD, int SHIFT = 1>
+__global__ __launch_bounds__(NT) void probe_blk(const uint8_t *in, long long in_bytes, int groups, int ntiles, uint32_t *sink) {
+    constexpr int SLOTB = 6144;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[RB * SLOTB + 256];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int tile = blockIdx.x;
+    if (XCD) {
+        const int q = ntiles >> 3, r = ntiles & 7, x = blockIdx.x & 7, i = blockIdx.x >> 3;
+        tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+    }
+    const long long col0 = (long long)tile * 128;
+    const int gf = (int)(col0 / NQ);
+    long long cl = col0 + 127;
+    if (cl > (long long)groups * NQ - 1) cl = (long long)groups * NQ - 1;
+    const int ng = (int)(cl / NQ) - gf + 1;
+    const long long base = (long long)gf * GSTRIDE;
+    const __amdgpu_buffer_rsrc_t rs = rsrc_of(in + base, in_bytes - base);
+    uint32_t voff[2];
+    bool act[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int i = (wave * 2 + h) * 64 + lane;
+        const int r = i / 88, j = i - r * 88;
+        voff[h] = r < ng ? (uint32_t)(r * GSTRIDE + 16 * j) : 0x80000000u;
+        act[h] = (wave * 2 + h) * 64 < ng * 88;  // uniform: a piece with any lane inside
+    }
+    auto issue = [&](int x) {
+        // SHIFT 1: chunks 16-byte aligned (odd blocks start 8 bytes early); 0: from the block start
+        // (odd blocks 8-misaligned); 2: every block 4 bytes past its start (all misaligned)
+        const uint32_t so = SHIFT == 1 ? (uint32_t)x * B - (uint32_t)(x & 1) * 8 : (uint32_t)x * B + (SHIFT == 2 ? 4u : 0u);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            if (act[h])
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void *)(ring + (x % RB) * SLOTB + (wave * 2 + h) * 1024), W,
+                                                         voff[h], so, 0, 0);
+    };
+    const int nis = (int)act[0] + (int)act[1];  // this wave's DMAs per step
+#pragma unroll
+    for (int x = 0; x < RB - 1; ++x) issue(x);
+    int nxt = RB - 1;
+    uint32_t acc = 0;
+    for (int x0 = 0; x0 < K; x0 += SB) {
+        if (nis == 2)
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * (RB - 1 - SB)) : "memory");
+        else if (nis == 1)
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(RB - 1 - SB) : "memory");
+        else
+            asm volatile("s_barrier" ::: "memory");
+        acc ^= *reinterpret_cast<const uint32_t *>(ring + (x0 % RB) * SLOTB + threadIdx.x * 20 + 3);
+        for (int t = 0; t < SB && nxt < K; ++t, ++nxt) issue(nxt);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (acc == 0x12345678u) sink[threadIdx.x] = acc;
+}
+
+// Round 5: what makes `blk` fast? Gather pieces (16 bytes = 4 columns of one sub-block, the last
+// chunk of a sub-block shifted back) over the tile's EXTENDED column range (every group the tile
+// touches, whole), XCD-aware tile order, 6 pieces per step:
+//   ORD 0: lanes over [sub-block][extended column] (the product's slot layout, 192 columns)
+//   ORD 1: lanes over (group, sub-block, chunk): each 1 KB piece walks a group's block nearly
+//          contiguously (like blk, but runs end at sub-block boundaries)
+// XCD false: plain tile order.
+template <int ORD, bool XCD>
+__global__ __launch_bounds__(NT) void probe_ext(const uint8_t *in, long long in_bytes, int groups, int ntiles, uint32_t *sink) {
+    constexpr int RB = 13, SB = 4, SLOTB = 6144;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[RB * SLOTB + 256];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int tile = blockIdx.x;
+    if (XCD) {
+        const int q = ntiles >> 3, r = ntiles & 7, x = blockIdx.x & 7, i = blockIdx.x >> 3;
+        tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+    }
+    const long long col0 = (long long)tile * 128;
+    const int gf = (int)(col0 / NQ);
+    long long cl = col0 + 127;
+    if (cl > (long long)groups * NQ - 1) cl = (long long)groups * NQ - 1;
+    const int ng = (int)(cl / NQ) - gf + 1;
+    const long long base = (long long)gf * GSTRIDE;
+    const __amdgpu_buffer_rsrc_t rs = rsrc_of(in + base, in_bytes - base);
+    uint32_t voff[2];
+    bool act[2];
+    constexpr int CPS = NQ / 4;  // chunks per sub-block (11)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int i = (wave * 2 + h) * 64 + lane;  // piece lane index 0..511
+        int r, a, c;
+        if (ORD == 0) {  // [a][ext column]: 48 chunks per sub-block row (192 columns)
+            a = i / 48;
+            const int cc = i - a * 48;  // chunk within the extended row
+            r = cc / CPS;
+            c = cc - r * CPS;
+        } else {  // (group, sub-block, chunk)
+            r = i / (8 * CPS);
+            const int t = i - r * 8 * CPS;
+            a = t / CPS;
+            c = t - a * CPS;
+        }
+        const int q = 4 * c;
+        const int co = 4 * q - (q >= NQ - 4 ? 4 * NQ - 175 : 0);
+        voff[h] = (r < ng && a < 8) ? (uint32_t)(r * GSTRIDE + a * 175 + co) : 0x80000000u;
+        act[h] = (wave * 2 + h) < 6;
+    }
+    auto issue = [&](int x) {
+        const uint32_t so = (uint32_t)x * B;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            if (act[h])
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void *)(ring + (x % RB) * SLOTB + (wave * 2 + h) * 1024), W,
+                                                         voff[h], so, 0, 0);
+    };
+    const int nis = (int)act[0] + (int)act[1];
+#pragma unroll
+    for (int x = 0; x < RB - 1; ++x) issue(x);
+    int nxt = RB - 1;
+    uint32_t acc = 0;
+    for (int x0 = 0; x0 < K; x0 += SB) {
+        if (nis == 2)
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * (RB - 1 - SB)) : "memory");
+        else if (nis == 1)
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(RB - 1 - SB) : "memory");
+        else
+            asm volatile("s_barrier" ::: "memory");
+        acc ^= *reinterpret_cast<const uint32_t *>(ring + (x0 % RB) * SLOTB + threadIdx.x * 20 + 3);
+        for (int t = 0; t < SB && nxt < K; ++t, ++nxt) issue(nxt);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (acc == 0x12345678u) sink[threadIdx.x] = acc;
+}
+
 int main(int argc, char **argv) {
     const int groups = argc > 1 ? atoi(argv[1]) : 8192;
     const long long bytes = (long long)groups * GSTRIDE;
@@ -153,6 +289,46 @@ int main(int argc, char **argv) {
             const double moved = (double)(mode == 1 || mode == 7 ? tiles_r : tiles_g) * K * 4096.0;  // DMA'd bytes
             printf("%-8s groups %d  best %.4f ms  %.0f GB/s DMA'd  %.0f GB/s of block bytes\n", names[mode], groups,
                    best, moved / best / 1e6, (double)groups * K * B / best / 1e6);
+        }
+    const char *en[4] = {"ext_ax", "ext_gx", "ext_a", "ext_g"};
+    for (int rep = 0; rep < 2; ++rep)
+        for (int mode = 0; mode < 4; ++mode) {
+            float best = 1e9f;
+            for (int it = 0; it < 10; ++it) {
+                CK(hipEventRecord(e0));
+                if (mode == 0) hipLaunchKernelGGL((probe_ext<0, true>), dim3(tiles_g), dim3(NT), 0, 0, in, bytes, groups, tiles_g, sink);
+                if (mode == 1) hipLaunchKernelGGL((probe_ext<1, true>), dim3(tiles_g), dim3(NT), 0, 0, in, bytes, groups, tiles_g, sink);
+                if (mode == 2) hipLaunchKernelGGL((probe_ext<0, false>), dim3(tiles_g), dim3(NT), 0, 0, in, bytes, groups, tiles_g, sink);
+                if (mode == 3) hipLaunchKernelGGL((probe_ext<1, false>), dim3(tiles_g), dim3(NT), 0, 0, in, bytes, groups, tiles_g, sink);
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                if (ms < best) best = ms;
+            }
+            printf("%-8s groups %d  best %.4f ms  %.0f GB/s of block bytes\n", en[mode], groups, best,
+                   (double)groups * K * B / best / 1e6);
+        }
+    const char *bn[6] = {"blk13s4x", "blk_nosh", "blk_mis4", "blk13s4", "blk8s2x", "blk16s4x"};
+    for (int rep = 0; rep < 2; ++rep)
+        for (int mode = 0; mode < 6; ++mode) {
+            float best = 1e9f;
+            for (int it = 0; it < 10; ++it) {
+                CK(hipEventRecord(e0));
+                if (mode == 0) hipLaunchKernelGGL((probe_blk<13, 4, true>), dim3(tiles_g), dim3(NT), 0, 0, in, bytes, groups, tiles_g, sink);
+                if (mode == 1) hipLaunchKernelGGL((probe_blk<13, 4, true, 0>), dim3(tiles_g), dim3(NT), 0, 0, in, bytes, groups, tiles_g, sink);
+                if (mode == 2) hipLaunchKernelGGL((probe_blk<13, 4, true, 2>), dim3(tiles_g), dim3(NT), 0, 0, in, bytes, groups, tiles_g, sink);
+                if (mode == 3) hipLaunchKernelGGL((probe_blk<13, 4, false>), dim3(tiles_g), dim3(NT), 0, 0, in, bytes, groups, tiles_g, sink);
+                if (mode == 4) hipLaunchKernelGGL((probe_blk<8, 2, true>), dim3(tiles_g), dim3(NT), 0, 0, in, bytes, groups, tiles_g, sink);
+                if (mode == 5) hipLaunchKernelGGL((probe_blk<16, 4, true>), dim3(tiles_g), dim3(NT), 0, 0, in, bytes, groups, tiles_g, sink);
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                if (ms < best) best = ms;
+            }
+            printf("%-8s groups %d  best %.4f ms  %.0f GB/s of block bytes\n", bn[mode], groups, best,
+                   (double)groups * K * B / best / 1e6);
         }
     return 0;
 }

@@ -140,7 +140,40 @@ class Body:
         have.add(name)
         return name
 
-    def emit(self, R, S, steps, KP, npf=0, st=0):
+    def unit_code(self, steps, unit, cur):
+        """The XOR code of one unit for this part (its rows' accumulators), as lines."""
+        save, self.lines = self.lines, []
+        L = self.lines
+        cols = [t for t in unit if steps[t][0] == "c"]
+        L.append("    {")
+        if "novalu" in ABLATE:  # keep the loaded words alive, do no XOR work
+            L.append("    asm volatile(\"\" :: " + ", ".join(f'"v"({cur}{a})' for a in range(8 * len(cols))) + ");")
+        elif cols and JOINT == 0:
+            self.window_step(steps[cols[0]][1], cur)
+        elif cols:
+            self.slp_unit([steps[t][1] for t in cols], cur)
+        for j, t in enumerate(unit):
+            st = steps[t]
+            if st[0] == "r" and self.y0 <= st[1] < self.y1:  # residual row y += the received block R_y
+                yi = st[1] - self.y0
+                for b in range(8):
+                    L.append(f"    XV(acc[{yi}][{b}], {cur}{8 * j + b});")
+        # Tie every accumulator to this unit (an empty volatile asm is a chained side effect):
+        # otherwise the DAG scheduler floats the pure bitop3 nodes of a ~30K-node basic block
+        # away from their loads and keeps every loaded word live.
+        for yi in range(self.y1 - self.y0):
+            L.append(f"    PIN8(acc[{yi}]);")
+        L.append("    }")
+        self.lines = save
+        return L
+
+    def emit(self, R, S, steps, KP, npf=0, st=0, group=None):
+        """group (SH_INTERLEAVE): the Body of every part; the wait / DMA / ring-read code is emitted
+        once and each unit's XOR code as an if-chain over the parts, so the part-waves of a
+        workgroup walk ONE region of code (each unit's parts adjacent) instead of P separate
+        straight-line functions: the instruction fetch of one wave prefetches its neighbours'
+        code (round 4: one code stream per workgroup, every part running part 0's code, was 12 %
+        faster -- the instruction supply's share)."""
         """Software-pipelined units (see fixed_common.hpp). A unit is JOINT consecutive input
         steps (a pair by default; recovery-row steps are single units) computed as one XOR
         program (tools/xor_sched.py); while unit u computes, the words of unit u+1 are read from
@@ -162,7 +195,7 @@ class Body:
             return st[1] if st[0] == "c" else KP + st[1]
 
         def uses(st):
-            return st[0] == "c" or self.y0 <= st[1] < self.y1
+            return st[0] == "c" or group is not None or self.y0 <= st[1] < self.y1
 
         units, i = [], 0
         while i < n:
@@ -262,26 +295,17 @@ class Body:
                     # keep the next unit's ds_reads at the top of the unit: left free, the
                     # scheduler sinks them to ~25 VALU before their use (LDS latency exposed)
                     L.append("    __builtin_amdgcn_sched_barrier(0);")
-            cols = [t for t in unit if steps[t][0] == "c"]
-            L.append("    {")
-            if "novalu" in ABLATE:  # keep the loaded words alive, do no XOR work
-                L.append("    asm volatile(\"\" :: " + ", ".join(f'"v"({cur}{a})' for a in range(8 * len(cols))) + ");")
-            elif cols and JOINT == 0:
-                self.window_step(steps[cols[0]][1], cur)
-            elif cols:
-                self.slp_unit([steps[t][1] for t in cols], cur)
-            for j, t in enumerate(unit):
-                st = steps[t]
-                if st[0] == "r" and uses(st):  # residual row y += the received recovery block R_y
-                    yi = st[1] - self.y0
-                    for b in range(8):
-                        L.append(f"    XV(acc[{yi}][{b}], {cur}{8 * j + b});")
-            # Tie every accumulator to this unit (an empty volatile asm is a chained side effect):
-            # otherwise the DAG scheduler floats the pure bitop3 nodes of a ~30K-node basic block
-            # away from their loads and keeps every loaded word live.
-            for yi in range(self.y1 - self.y0):
-                L.append(f"    PIN8(acc[{yi}]);")
-            L.append("    }")
+            if group is None:
+                L.extend(self.unit_code(steps, unit, cur))
+            else:
+                chain = [(pi, b.unit_code(steps, unit, cur)) for pi, b in enumerate(group)]
+                # parts with XOR work in this unit (decode's recovery-row steps touch one part)
+                chain = [(pi, c) for pi, c in chain
+                         if any(l.strip() not in ("{", "}") and not l.strip().startswith("PIN8") for l in c)]
+                for ci, (pi, c) in enumerate(chain):
+                    kw = "if" if ci == 0 else "else if"
+                    L.append(f"    {kw} (part == {pi})")
+                    L.extend(c)
             if READ_LATE and u + 1 < len(units):
                 # the next unit's words are read after this unit's XORs (its words are dead
                 # then): the two banks are never live together
@@ -355,7 +379,17 @@ class Body:
 # search costs ~0.1 s per 16-bit unit, ~2,600 units over CONFIGS.
 JOINT = int(os.environ.get("SH_JOINT", "2"))  # steps per XOR program; 0 = the reference's window tables
 _SCHED = {}
-_CACHE = os.path.join(ROOT, "shorthair_amd", "csrc", "gen_cache", "xor_sched_v2.json")  # v2: 6-trial joint search
+
+
+def _sched_hash():
+    """The cache file is keyed by the scheduler's source: a change to tools/xor_sched.py starts a
+    fresh cache instead of reusing programs the old search produced."""
+    import hashlib
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "xor_sched.py"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:12]
+
+
+_CACHE = os.path.join(ROOT, "shorthair_amd", "csrc", "gen_cache", f"xor_sched_{_sched_hash()}.json")
 
 
 def unit_steps(R, rows):
@@ -371,13 +405,40 @@ def _sched_key(tg, nbits):
     return f"{nbits}:" + ",".join(f"{t:x}" for t in tg)
 
 
+def check_program(tg, nbits, inters, reps):
+    """A (cached) XOR program must be exact: every intermediate is the XOR of its 2-3 operands,
+    each operand an input word (one bit) or an earlier intermediate, and every target's
+    representation XORs to the target. A corrupt cache entry would otherwise become a wrong
+    kernel that only the GPU goldens catch."""
+    have = {1 << a for a in range(nbits)}
+    for w, ops in inters:
+        acc = 0
+        assert len(ops) in (2, 3), "intermediate arity"
+        for o in ops:
+            assert o in have, "operand not yet available"
+            acc ^= o
+        assert acc == w, "intermediate is not the XOR of its operands"
+        have.add(w)
+    for t in tg:
+        if not t:
+            continue
+        acc = 0
+        for w in reps[t]:
+            assert w in have, "representation uses an unknown word"
+            acc ^= w
+        assert acc == t, "representation does not XOR to its target"
+
+
 def sched(tg, nbits):
     key = _sched_key(tg, nbits)
     if key not in _SCHED:
         import xor_sched
         _SCHED[key] = xor_sched.compute_key(key)[1]
     inters, reps = _SCHED[key]
-    return [(w, tuple(ops)) for w, ops in inters], {int(t): tuple(r) for t, r in reps.items()}
+    inters = [(w, tuple(ops)) for w, ops in inters]
+    reps = {int(t): tuple(r) for t, r in reps.items()}
+    check_program(tg, nbits, inters, reps)
+    return inters, reps
 
 
 def load_sched_cache():
@@ -518,6 +579,9 @@ def gen_config(k, m):
     for mode in ("enc", "dec"):
         rinit = mode == "dec" and RINIT and not pers[mode]
         steps = [("c", x) for x in range(k)] + ([("r", y) for y in range(m)] if mode == "dec" and not rinit else [])
+        if INTERLEAVE and not pers[mode] and not rinit and len(parts) > 1:
+            out.extend(interleaved_function(name, mode, k, rows, parts, R, sync, steps, KP))
+            continue
         for p, (y0, y1) in enumerate(parts):
             # epilogue stores per wave: two 16-byte pieces per row of its part (RowSink::row)
             npf = R - 2 * P if pers[mode] else 0
@@ -583,6 +647,41 @@ def gen_config(k, m):
                        f"{'false' if 'nodma' in ABLATE else 'true'}, {'true' if stream_mode(P) else 'false'})\n"))
         paths.append(path)
     return paths
+
+
+INTERLEAVE = os.environ.get("SH_INTERLEAVE", "0") == "1"
+
+
+def interleaved_function(name, mode, k, rows, parts, R, sync, steps, KP):
+    """run_<name>_<mode>(part, src, sink) as ONE function: the ring code once, each unit's XOR
+    code an if-chain over the parts (Body.emit group=...), the epilogue's rows by part."""
+    nrmax = max(b - a for a, b in parts)
+    bodies = [Body(k, rows, y0, y1, nrmax) for y0, y1 in parts]
+    body = bodies[0].emit(R, sync, steps, KP, group=bodies)
+    base, extra = divmod(sum(b - a for a, b in parts), len(parts))
+    out = ["template <class Src, class Snk>",
+           f"__device__ __forceinline__ void run_{name}_{mode}(int part, const Src &src, const Snk &sink) {{",
+           f"    uint32_t acc[{nrmax}][8];",
+           f"    for (int y = 0; y < {nrmax}; ++y) for (int b = 0; b < 8; ++b) ZERO(acc[y][b]);",
+           body,
+           "    __builtin_amdgcn_sched_barrier(0);",
+           "    // epilogue: this part's rows (part p owns rows y0(p) .. y0(p) + nr(p) - 1)",
+           "    src.release();  // the store scratch aliases the ring",
+           "    sink.prepare();",
+           f"    const int y0 = part * {base} + (part < {extra} ? part : {extra});",
+           f"    const int nr = {base} + (part < {extra} ? 1 : 0);"]
+    for yi in range(nrmax):  # every part joins the same number of row barriers
+        out.append("    __builtin_amdgcn_sched_barrier(0);")
+        if "nostore" in ABLATE:
+            out.append(f"    asm volatile(\"\" :: " + ", ".join(f'"v"(acc[{yi}][{b}])' for b in range(8)) + ");")
+        elif all(b - a > yi for a, b in parts):
+            out.append(f"    sink.template row<{yi}>(y0 + {yi}, acc[{yi}]);")
+        else:
+            out.append(f"    if ({yi} < nr) sink.template row<{yi}>(y0 + {yi}, acc[{yi}]);")
+            out.append(f"    else sink.template pad<{yi}>();")
+    out.append("}")
+    out.append("")
+    return out
 
 
 # Snippet table for runtime coefficients (decode stage B, csrc/stageb.hip): snippet c computes

@@ -29,6 +29,7 @@ for s in "$@"; do
         echo "== variant $v"
         SH_LIB_PATH=$L timeout -k 10 120 python tools/run_ops.py --op both --iters 10 2>&1 | grep -v amdgpu.ids || exit 1
       done ;;
+    env:*) bash tools/gpu_envab.sh "$(echo ${s#env:} | tr + " ")" || exit 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
