@@ -398,7 +398,8 @@ def unit_steps(R, rows):
     (28,4) ring has 4), and registers: 8 accumulators per row + the pair's 16 words + its ~20
     live intermediates fit 128 VGPRs up to 8 rows ((190,66)'s 9-row parts spill with pairs; a
     scratch spill's vmcnt wait would also drain the DMA ring)."""
-    return 2 if JOINT == 2 and R >= 8 and rows <= 8 else 1
+    pair_rows = int(os.environ.get("SH_PAIR_ROWS", "8"))  # 16: pairs for 16-row parts (2 waves/SIMD)
+    return 2 if JOINT == 2 and R >= 8 and rows <= pair_rows else 1
 
 
 def _sched_key(tg, nbits):
