@@ -681,8 +681,13 @@ inline int persistent_slots() {
     return 2 * cus;  // a multiple of 8 on MI355X (256 CUs)
 }
 
+// Measurement builds only (SH_HSACO_DIR, fixed_dispatch.cpp): launch the kernel `tag` from a
+// code object of that directory instead (tools/il_reorder.py layouts); *used = false: none.
+hipError_t module_launch(const char *tag, const FixedArgs &a, unsigned blocks, unsigned threads, size_t lds,
+                         hipStream_t s, bool *used);
+
 template <class S, bool DEC, bool STREAM = false, bool PERS = false>
-inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArgs)) {
+inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArgs), const char *tag = nullptr) {
     constexpr bool dec = DEC;
     a.groups_per_wg = (S::COLS - 1) / a.geo.nq + 2;
     // ring (the row images of the epilogue alias it); a streaming source needs only the images
@@ -693,6 +698,11 @@ inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArg
     const long long cols = static_cast<long long>(a.groups) * a.geo.nq;
     unsigned blocks = static_cast<unsigned>((cols + S::COLS - 1) / S::COLS);  // one tile each
     if (PERS) blocks = std::min<unsigned>(blocks, static_cast<unsigned>(persistent_slots()));
+    if (tag) {
+        bool used = false;
+        const hipError_t e = module_launch(tag, a, blocks, S::NT, lds, s, &used);
+        if (used) return e;
+    }
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(S::NT), lds, s, a);
     return hipGetLastError();
 }
@@ -718,7 +728,7 @@ inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArg
         run_##NAME##_##MODE(part, src, sink);                                                     \
     }                                                                                             \
     hipError_t launch_##NAME##_##MODE(FixedArgs a, hipStream_t s) {                               \
-        return launch_shape<Shape<K, M, P, CW, R, DMA>, DEC, STREAM>(a, s, kern_##NAME##_##MODE); \
+        return launch_shape<Shape<K, M, P, CW, R, DMA>, DEC, STREAM>(a, s, kern_##NAME##_##MODE, #NAME "_" #MODE); \
     }                                                                                             \
     }                                                                                             \
     }

@@ -1,6 +1,12 @@
 // Dispatch to the compile-time-scheduled kernels generated for specific (k, m).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <string>
+
 #include "fixed_configs.h"  // from the generated-kernel directory (-I, see build.py)
 #include "kernels.hpp"
 
@@ -11,6 +17,43 @@ namespace fixed {
     hipError_t launch_k##K##_m##M##_dec(FixedArgs a, hipStream_t s);
 SH_FIXED_CONFIGS(SH_DECL)
 #undef SH_DECL
+
+// Measurement builds: SH_HSACO_DIR=<dir> makes every compile-time kernel whose code object
+// <dir>/<tag>.hsaco exists (tag = k<k>_m<m>_<enc|dec>, e.g. a tools/il_reorder.py layout of the
+// same kernel) launch from that code object. Not used by the product (the variable is unset).
+hipError_t module_launch(const char *tag, const FixedArgs &a, unsigned blocks, unsigned threads, size_t lds,
+                         hipStream_t s, bool *used) {
+    *used = false;
+    static const char *dir = std::getenv("SH_HSACO_DIR");
+    if (!dir) return hipSuccess;
+    static std::mutex mu;
+    static std::map<std::string, hipFunction_t> fns;
+    hipFunction_t f = nullptr;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = fns.find(tag);
+        if (it == fns.end()) {
+            hipModule_t mod = nullptr;
+            const std::string path = std::string(dir) + "/" + tag + ".hsaco";
+            const std::string kname = std::string("kern_") + tag;
+            const std::string sym = "_ZN2sh5fixed" + std::to_string(kname.size()) + kname + "ENS_9FixedArgsE";
+            if (hipModuleLoad(&mod, path.c_str()) != hipSuccess || hipModuleGetFunction(&f, mod, sym.c_str()) != hipSuccess) {
+                f = nullptr;
+                (void)hipGetLastError();
+            } else {
+                std::fprintf(stderr, "libcauchy256: %s from %s\n", sym.c_str(), path.c_str());
+            }
+            it = fns.emplace(tag, f).first;
+        }
+        f = it->second;
+    }
+    if (!f) return hipSuccess;
+    *used = true;
+    FixedArgs arg = a;
+    size_t sz = sizeof(arg);
+    void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &arg, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+    return hipModuleLaunchKernel(f, blocks, 1, 1, threads, 1, 1, static_cast<unsigned>(lds), s, nullptr, cfg);
+}
 }  // namespace fixed
 
 bool has_fixed(int k, int m, int B) {

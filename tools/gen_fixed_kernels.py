@@ -114,8 +114,9 @@ def row_bytes(c):
 class Body:
     """Straight-line code for one part (rows y0..y1-1) over all k inputs."""
 
-    def __init__(self, k, rows, y0, y1, rows_max=None):
+    def __init__(self, k, rows, y0, y1, rows_max=None, part=0):
         self.k, self.rows, self.y0, self.y1 = k, rows, y0, y1
+        self.part = part
         self.rows_max = rows_max or (y1 - y0)  # the largest part of the kernel (one unit size for all)
         self.lines = []
 
@@ -261,6 +262,8 @@ class Body:
             cur, nxt = ("dA", "dB") if u % 2 == 0 else ("dB", "dA")
             L.append("    // ---- " + ", ".join(f"step {t}: " + (f"input block {steps[t][1]}" if steps[t][0] == "c"
                                                                   else f"recovery row {steps[t][1]}") for t in unit))
+            if IL_MARK and group is None:  # chunk marker for tools/il_reorder.py (an asm comment)
+                L.append(f'    asm volatile(";shu {self.part} {u}");')
             # Pin the unit structure: without this hipcc hoists work across units.
             L.append("    __builtin_amdgcn_sched_barrier(0);")
             if u + 1 < len(units):
@@ -311,6 +314,9 @@ class Body:
                 # then): the two banks are never live together
                 L.append("    __builtin_amdgcn_sched_barrier(0);")
                 read_unit(u + 1, nxt)
+        if IL_MARK and group is None:
+            L.append("    __builtin_amdgcn_sched_barrier(0);")
+            L.append(f'    asm volatile(";shu {self.part} end");')
         return "\n".join(L)
 
     def window_step(self, x, cur):
@@ -586,7 +592,7 @@ def gen_config(k, m):
         for p, (y0, y1) in enumerate(parts):
             # epilogue stores per wave: two 16-byte pieces per row of its part (RowSink::row)
             npf = R - 2 * P if pers[mode] else 0
-            body = Body(k, rows, y0, y1, max(b - a for a, b in parts)).emit(R, sync, steps, KP, npf=npf,
+            body = Body(k, rows, y0, y1, max(b - a for a, b in parts), part=p).emit(R, sync, steps, KP, npf=npf,
                                                                             st=2 * (y1 - y0))
             nr = y1 - y0
             out.append(f"template <class Src, class Snk>")
@@ -651,6 +657,8 @@ def gen_config(k, m):
 
 
 INTERLEAVE = os.environ.get("SH_INTERLEAVE", "0") == "1"
+# Unit markers (asm comments ";shu <part> <unit>") for the code-layout pass tools/il_reorder.py
+IL_MARK = os.environ.get("SH_IL_MARK", "0") == "1"
 
 
 def interleaved_function(name, mode, k, rows, parts, R, sync, steps, KP):
