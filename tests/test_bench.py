@@ -121,3 +121,25 @@ def test_bench_uneven_shards_default_chunk():
     rr = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])["root_resident"]
     assert rr.get("roundtrip_ok") is True, rr
     assert rr["encode"]["chunk_groups_per_rank"] == 70 and rr["encode"]["chunks"] == 3
+
+
+def test_sweep_regression_check(tmp_path):
+    """tools/sweep_table.py --against flags a sweep row or headline op that got slower (VERDICT r4 #3)."""
+    import importlib.util
+    import json
+    spec = importlib.util.spec_from_file_location("sweep_table", os.path.join(ROOT, "tools", "sweep_table.py"))
+    st = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(st)
+    row = {"config": "C4", "k": 28, "m": 4, "B": 256, "groups": 209263, "path": "fixed",
+           "encode_ms": 0.35, "decode_ms": 0.705, "decode_frac": 0.1, "mean_e": 4.0}
+    old = {"value": 1.0, "unit": "GiB/s", "ops": {"encode_ms": 0.68, "decode_ms": 1.08}, "sweep": [row]}
+    new = json.loads(json.dumps(old))
+    new["sweep"][0]["decode_ms"] = 0.765  # 8.5 % slower
+    regs, n = st.compare(new, old, 0.05)
+    assert n == 4 and [r[0] for r in regs] == ["C4 (28,4,256) G=209263 fixed decode"]
+    assert st.compare(new, old, 0.10)[0] == []
+    a, b = tmp_path / "old.json", tmp_path / "new.json"
+    a.write_text(json.dumps(old) + "\n")
+    b.write_text("log line\n" + json.dumps(new) + "\n")
+    assert st.main([str(b), "--against", str(a)]) == 1
+    assert st.main([str(a), "--against", str(a)]) == 0

@@ -8,7 +8,7 @@
 set -u
 TAG=${1:?tag}
 mkdir -p gpurun_out
-IFETCH="SQC_ICACHE_REQ SQC_ICACHE_MISSES SQC_TC_INST_REQ SQC_ICACHE_BUSY_CYCLES" PROFDIR=profiles/r04 \
+IFETCH="SQC_ICACHE_REQ SQC_ICACHE_MISSES SQC_TC_INST_REQ SQC_ICACHE_BUSY_CYCLES" PROFDIR=profiles/r05 \
   bash tools/gpu_profile.sh "$TAG" > "gpurun_out/prof_$TAG.out" 2>&1 || { tail -5 "gpurun_out/prof_$TAG.out"; exit 1; }
 tail -3 "gpurun_out/prof_$TAG.out"
 timeout -k 10 600 python bench.py > "gpurun_out/bench_full_$TAG.json" 2> "gpurun_out/bench_full_$TAG.err" || { tail -5 "gpurun_out/bench_full_$TAG.err"; exit 1; }
