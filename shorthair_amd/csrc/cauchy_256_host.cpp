@@ -401,9 +401,17 @@ hipError_t launch_fixed_batch(int k, int m, int B, int groups, const uint8_t *in
 }
 
 // Step slices of the single-group latency path: the k (+ m) serial ring steps of one group are
-// split over up to 8 workgroups, each XOR-ing its steps' products into a partial output, and the
-// partials are XOR-reduced (the products are linear). ~25 steps per slice.
-int latency_slices(int nsteps) { return std::max(1, std::min(8, nsteps / 25)); }
+// split over up to 32 workgroups, each XOR-ing its steps' products into a partial output, and the
+// partials are XOR-reduced (the products are linear). >= 6 steps per slice.
+constexpr int kSliceCap = 32;  // slice_scratch holds this many partial outputs
+int latency_slices(int nsteps) {
+    // SH_SLICE_MAX / SH_SLICE_STEPS: measurement switches (slices at most, steps per slice at least)
+    // (200,32,1400) single-group calls: 8 x 25 steps 80 / 112 us (encode / decode), 16 x 12 74 / 104,
+    // 32 x 6 70 / 104 (profiles/r05/ab_runs.txt block 13)
+    static const int mx = std::getenv("SH_SLICE_MAX") ? std::atoi(std::getenv("SH_SLICE_MAX")) : 32;
+    static const int st = std::getenv("SH_SLICE_STEPS") ? std::atoi(std::getenv("SH_SLICE_STEPS")) : 6;
+    return std::max(1, std::min(std::min(mx, kSliceCap), nsteps / std::max(st, 1)));
+}
 
 // One pass of the tile kernels over the batch (encode, or decode stage A with position tables).
 // slice_scratch (groups == 1 only): room for latency_slices() partial outputs of m * B bytes;
@@ -458,7 +466,7 @@ int launch_tile_batch(Context &c, int k, int m, int B, int groups, const uint8_t
 }
 
 // ---- batched encode ----
-// slice_scratch (single-group ABI): 8 * m * B device bytes that let one group's steps run as
+// slice_scratch (single-group ABI): kSliceCap * m * B device bytes that let one group's steps run as
 // parallel slices on the tile kernels (latency); nullptr = the throughput kernels.
 int encode_batch(int k, int m, int B, int groups, const uint8_t *d_in, uint8_t *d_out,
                  hipStream_t s, uint8_t *slice_scratch = nullptr) {
@@ -646,9 +654,11 @@ int dec_chunks(int groups) {
 
 // Common decode core (m >= 2, valid params): writes recovered blocks densely into `dst`
 // ([G][emax][B]) and leaves per-group e / rec_idx / erasures in the workspace.
+// host_setup: the workspace's setup fields were written by the host (single-group ABI,
+// host_decode_setup below) and arrive with the blocks: no setup kernel.
 int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_blocks,
                 const uint8_t *d_rows, DecodeWS &w, int *errors, uint8_t *dst, hipStream_t s,
-                uint8_t *slice_scratch = nullptr) {
+                uint8_t *slice_scratch = nullptr, bool host_setup = false) {
     uint8_t *gen = generator(c, k, m);
     if (!gen) return -2;
     sh::DecodeSetupArgs sa{};
@@ -688,7 +698,7 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
         }
     }
     if (ev) SH_CHECK(hipEventRecord(ev[0], s));
-    SH_CHECK(sh::launch_decode_setup(sa, groups, s));
+    if (!host_setup) SH_CHECK(sh::launch_decode_setup(sa, groups, s));
     if (ev) SH_CHECK(hipEventRecord(ev[1], s));
 
     const Geometry geo = sh::make_geometry(B);
@@ -778,14 +788,67 @@ int invalid_decode_status(int k, int groups, const uint8_t *d_rows, hipStream_t 
     return 0;
 }
 
+// Host restatement of decode_setup (kernels.hip) for one group, written into a host image of the
+// workspace carved exactly as the device's (carve()): the single-group ABI uploads it with the
+// blocks, so its decode runs no setup kernel. Covers the modes whose stage B takes byte
+// coefficients (stageb_v2, stageb_small) after a full-residual stage A, for m >= 7 (closed-form
+// Cauchy inverse, kernels.hip decode_setup: S^-1[j][i] = a_j b_i / (x_j (x_j + y_i))); returns
+// false (device setup) otherwise. rec[i]: array index of the i-th recovery block, era[j]: j-th
+// erased original row (sort_blocks order, cauchy_256.cpp:522-554), 0 < e <= number of erasures.
+bool host_decode_setup(const DecodeWS &w, int k, int m, const uint8_t *rows, int e, const int *rec,
+                       const int *era) {
+    if (!w.fixed || !(w.v2 || w.small) || m < 7 || !w.coefB || !w.rrow || !w.pos || !w.rpos) return false;
+    const sh::GF256 &f = sh::gf();
+    std::vector<uint8_t> xp, yp;
+    sh::cauchy_params(k, m, xp, yp);
+    *w.e = e;
+    std::memset(w.rrow, 0, round4(w.emax));
+    std::memset(w.pos, 0xFF, round4(k));
+    std::memset(w.rpos, 0xFF, round4(m));
+    for (int j = 0; j < k; ++j) {
+        if (rows[j] < k) w.pos[rows[j]] = static_cast<uint8_t>(j);
+        else w.rpos[rows[j] - k] = static_cast<uint8_t>(j);
+    }
+    int x[256], y[256], la[256], lb[256];
+    for (int t = 0; t < e; ++t) {
+        w.rec_idx[t] = static_cast<uint8_t>(rec[t]);
+        w.erasures[t] = static_cast<uint8_t>(era[t]);
+        w.rrow[t] = static_cast<uint8_t>(rows[rec[t]] - k);
+        x[t] = xp[era[t]];
+        y[t] = yp[rows[rec[t]] - k];
+    }
+    auto mod255 = [](int v) { v %= 255; return v < 0 ? v + 255 : v; };
+    for (int t = 0; t < e; ++t) {
+        int a = 0, b = 0;
+        for (int q = 0; q < e; ++q) {
+            a += f.log[x[t] ^ y[q]];
+            b += f.log[x[q] ^ y[t]];
+            if (q != t) {
+                a -= f.log[x[t] ^ x[q]];
+                b -= f.log[y[t] ^ y[q]];
+            }
+        }
+        la[t] = mod255(a - f.log[x[t]]);
+        lb[t] = mod255(b);
+    }
+    std::memset(w.coefB, 0, static_cast<size_t>(w.emax) * w.ldB);  // [i][j] = S^-1[j][i], zero past e
+    for (int i = 0; i < e; ++i)
+        for (int j = 0; j < e; ++j)
+            w.coefB[static_cast<size_t>(i) * w.ldB + j] = f.exp[mod255(la[j] + lb[i] - f.log[x[j] ^ y[i]])];
+    return true;
+}
+
 // e_host (optional, pinned host memory): receives group 0's e, copied on `s` while the workspace
 // is still leased to this call (the single-group ABI reads it after synchronising).
 // h_dense (single-group ABI, optional): the e_dense recovered rows of group 0 are copied densely
 // into this pinned buffer instead of being scattered on the device (the caller knows the
 // recovery positions and places them itself).
+// ws_ext (single-group ABI, optional): the workspace, carved by the caller in its staging
+// buffer (no lease); host_setup: its setup fields are already there (decode_core).
 int decode_batch(int k, int m, int B, int groups, uint8_t *d_blocks, uint8_t *d_rows,
                  hipStream_t s, int *e_host = nullptr, uint8_t *slice_scratch = nullptr,
-                 uint8_t *h_dense = nullptr, int e_dense = 0) {
+                 uint8_t *h_dense = nullptr, int e_dense = 0, uint8_t *ws_ext = nullptr,
+                 bool host_setup = false) {
     Context &c = ctx();
     DeviceScope ds(c);
     if (ds.rc) return ds.rc;
@@ -801,10 +864,15 @@ int decode_batch(int k, int m, int B, int groups, uint8_t *d_blocks, uint8_t *d_
     if (k + m > 256 || B % 8 != 0) return invalid_decode_status(k, groups, d_rows, s);
     DecodeWS w{};
     WsLease ls;
-    // slice_scratch: the single-group ABI (a staging stream, no batch reserve)
-    if (int rc = lease_workspace(c, s, carve(w, nullptr, k, m, B, groups, true), ls, slice_scratch == nullptr)) return rc;
-    carve(w, ls.p, k, m, B, groups, true);
-    if (int rc = decode_core(c, k, m, B, groups, d_blocks, d_rows, w, ls.errors, w.recovered, s, slice_scratch))
+    if (ws_ext) {
+        carve(w, ws_ext, k, m, B, groups, true);
+    } else {
+        // slice_scratch: the single-group ABI (a staging stream, no batch reserve)
+        if (int rc = lease_workspace(c, s, carve(w, nullptr, k, m, B, groups, true), ls, slice_scratch == nullptr)) return rc;
+        carve(w, ls.p, k, m, B, groups, true);
+    }
+    if (int rc = decode_core(c, k, m, B, groups, d_blocks, d_rows, w, ws_ext ? nullptr : ls.errors, w.recovered, s,
+                             slice_scratch, host_setup))
         return rc;
     if (h_dense) {  // still under the workspace lease: the copy is ordered before any regrowth
         SH_CHECK(hipMemcpyAsync(h_dense, w.recovered, static_cast<size_t>(e_dense) * B, hipMemcpyDeviceToHost, s));
@@ -1117,7 +1185,7 @@ extern "C" int cauchy_256_encode(int k, int m, const unsigned char *data_ptrs[],
     SlotLease sl(c);
     if (sl.rc) return sl.rc;
     StageSlot &st = *sl.s;
-    const size_t scratch = 8 * out_bytes;  // step-slice partials (latency path)
+    const size_t scratch = kSliceCap * out_bytes;  // step-slice partials (latency path)
     if (int rc = st.h.ensure(in_bytes + out_bytes)) return rc;
     if (int rc = st.d.ensure(in_bytes + out_bytes + scratch, st.stream)) return rc;
     uint8_t *h = static_cast<uint8_t *>(st.h.p);
@@ -1165,21 +1233,30 @@ extern "C" int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes) {
     SlotLease sl(c);
     if (sl.rc) return sl.rc;
     StageSlot &st = *sl.s;
-    const size_t scratch = 8 * static_cast<size_t>(std::max(m, 1)) * block_bytes;  // step-slice partials
-    if (int rc = st.h.ensure(data_bytes + 256 + 8)) return rc;
-    if (int rc = st.d.ensure(data_bytes + 256 + scratch, st.stream)) return rc;
+    const size_t scratch = kSliceCap * static_cast<size_t>(std::max(m, 1)) * block_bytes;  // step-slice partials
+    // staging: [blocks][rows (256)][workspace (general path)][slice partials]
+    const size_t ws_off = (data_bytes + 256 + 255) & ~static_cast<size_t>(255);
+    DecodeWS probe{};
+    const size_t ws_bytes = general ? carve(probe, nullptr, k, m, block_bytes, 1, true) : 0;
+    if (int rc = st.h.ensure(ws_off + ws_bytes + 8)) return rc;
+    if (int rc = st.d.ensure(ws_off + ws_bytes + scratch, st.stream)) return rc;
     uint8_t *h = static_cast<uint8_t *>(st.h.p);
     uint8_t *d = static_cast<uint8_t *>(st.d.p);
     for (int i = 0; i < k; ++i) {
         std::memcpy(h + static_cast<size_t>(i) * block_bytes, blocks[i].data, block_bytes);
         h[data_bytes + i] = blocks[i].row;
     }
-    SH_CHECK(hipMemcpyAsync(d, h, data_bytes + k, hipMemcpyHostToDevice, st.stream));
     if (general) {
-        // the recovered rows come back densely (e blocks, no device scatter kernel) and are placed
-        // here: VERDICT r4 #9, the whole group went both ways
+        // The decode setup runs here (host_decode_setup) where it applies: its workspace fields
+        // go up with the blocks in one copy, and the recovered rows come back densely (e blocks,
+        // no device scatter kernel) to be placed here.
+        DecodeWS wh{};
+        carve(wh, h + ws_off, k, m, block_bytes, 1, true);
+        const bool hs = host_decode_setup(wh, k, m, h + data_bytes, e, rec, era);
+        const size_t up = hs ? ws_off + static_cast<size_t>(wh.residual - (h + ws_off)) : data_bytes + k;
+        SH_CHECK(hipMemcpyAsync(d, h, up, hipMemcpyHostToDevice, st.stream));
         const int rc = decode_batch(k, m, block_bytes, 1, d, d + data_bytes, st.stream, nullptr,
-                                    d + data_bytes + 256, h, e);
+                                    d + ws_off + ws_bytes, h, e, d + ws_off, hs);
         if (rc != 0) return rc;
         SH_CHECK(hipStreamSynchronize(st.stream));
         for (int l = 0; l < e; ++l) {
@@ -1188,6 +1265,7 @@ extern "C" int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes) {
         }
         return 0;
     }
+    SH_CHECK(hipMemcpyAsync(d, h, data_bytes + k, hipMemcpyHostToDevice, st.stream));
     // m == 1 (cauchy_decode_m1) and the parameter-error paths: the batch decode in place
     int *e_host = reinterpret_cast<int *>(h + ((data_bytes + k + 3) & ~static_cast<size_t>(3)));
     *e_host = 0;

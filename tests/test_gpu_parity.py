@@ -107,6 +107,35 @@ def test_single_group_decode_abi(sh, c):
     assert np.array_equal(out, vectors()[c["name"] + "_out"])
 
 
+@pytest.mark.parametrize("k,m,B", [(200, 32, 1400), (64, 16, 1400), (150, 40, 1352), (28, 8, 256),
+                                   (100, 20, 512), (190, 66, 1336), (12, 7, 64)])
+def test_single_group_decode_random_patterns(sh, k, m, B):
+    """cauchy_256_decode (host-side setup for m >= 7) on random erasure sets: e = 1..min(k, m) lost
+    originals, a random subset of e recovery rows, blocks in random array order; results and rows
+    against the oracle's decode of the same array."""
+    ora = po.oracle()
+    rng = np.random.default_rng(k * 1000 + m)
+    data = po.fill_group(k + m, k, B, 0x5A)
+    rc, rec = ora.encode(k, m, data, B)
+    assert rc == 0
+    whole = np.concatenate([data, rec])
+    for trial in range(6):
+        e = int(rng.integers(1, min(k, m) + 1)) if trial else min(k, m)
+        lost = rng.choice(k, size=e, replace=False)
+        recv = k + rng.choice(m, size=e, replace=False)
+        rows = np.array(sorted(set(range(k)) - set(lost.tolist())) + recv.tolist())
+        rng.shuffle(rows)
+        bufs = [whole[r].copy() for r in rows]
+        ref = [whole[r].copy() for r in rows]
+        rc_ref, rows_ref = ora.decode(k, m, ref, rows.tolist(), B)
+        arr = (sh.Block * k)(*[sh.Block(b.ctypes.data, int(r)) for b, r in zip(bufs, rows)])
+        assert sh.cauchy_256_decode(k, m, arr, B) == rc_ref == 0
+        assert [arr[i].row for i in range(k)] == rows_ref
+        for i in range(k):
+            assert np.array_equal(bufs[i], ref[i]), (trial, i)
+            assert np.array_equal(bufs[i], data[rows_ref[i]])
+
+
 def test_single_group_abi_concurrent(sh):
     """Single-group calls from several threads at once (two Shorthair codec objects on two threads):
     each call holds its own staging slot and stream, so the calls overlap and none sees another's
