@@ -579,7 +579,17 @@ size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool n
     return off;
 }
 
-hipError_t launch_stage_b(const DecodeWS &w, int n_in, int B, int groups, uint8_t *dst, hipStream_t s) {
+// Rows per stage-B slice on the single-group latency path (SH_SB_SLICE, measurement switch; 0 = one
+// workgroup streams all e rows).
+int stageb_row_slice() {
+    static const int n = std::getenv("SH_SB_SLICE") ? std::atoi(std::getenv("SH_SB_SLICE")) : 8;
+    return std::max(0, n);
+}
+
+// slice_scratch (groups == 1, stageb_v2 only): the e input rows are split into slices of
+// stageb_row_slice() rows, one workgroup each, whose partial outputs are XOR-reduced into dst.
+hipError_t launch_stage_b(const DecodeWS &w, int n_in, int B, int groups, uint8_t *dst, hipStream_t s,
+                          uint8_t *slice_scratch = nullptr) {
     if (w.small) {
         sh::StageBSmallArgs f{};
         f.in = w.residual;
@@ -613,6 +623,15 @@ hipError_t launch_stage_b(const DecodeWS &w, int n_in, int B, int groups, uint8_
         f.groups = groups;
         f.geo = sh::fixed_geometry(B);
         f.snip_base = ctx().snip_base;
+        const int rs = stageb_row_slice();
+        if (slice_scratch && groups == 1 && rs > 0 && w.emax > rs) {
+            f.row_slice = rs;
+            f.row_slices = (w.emax + rs - 1) / rs;
+            f.out_slice_bytes = f.out_gstride;
+            f.out = slice_scratch;
+            if (hipError_t r = sh::launch_stageb_v2(f, s)) return r;
+            return sh::launch_xor_reduce(slice_scratch, f.out_gstride, f.row_slices, dst, f.out_gstride, s);
+        }
         return sh::launch_stageb_v2(f, s);
     }
     if (w.fixed) {
@@ -752,7 +771,7 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
         }
         if (ev) SH_CHECK(hipEventRecord(ev[2], s));
         // Stage B: recovered_j = sum_y M(S^-1[j][i(y)]) residual_y over the received rows y
-        SH_CHECK(launch_stage_b(w, m, B, groups, dst, s));
+        SH_CHECK(launch_stage_b(w, m, B, groups, dst, s, groups == 1 ? slice_scratch : nullptr));
         if (ev) SH_CHECK(hipEventRecord(ev[3], s));
         return 0;
     }

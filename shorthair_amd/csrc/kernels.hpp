@@ -124,6 +124,12 @@ struct StageBV2Args {
     Geometry geo;
     uint64_t snip_base;       // address of snippet 0 of the accumulating table (stride SNIP_STRIDE)
     int j_base;               // set by the launcher: first output of the launch (a tail launch)
+    // Row slices (single-group latency path; 0 = off): workgroup z applies input rows
+    // [z * row_slice, min(e, (z + 1) * row_slice)) and writes its partial output at
+    // out + z * out_slice_bytes; the caller XOR-reduces the partials.
+    int row_slice;
+    int row_slices;
+    long long out_slice_bytes;
 };
 bool stageb_v2_ok(const Geometry &geo, int emax);
 hipError_t launch_stageb_v2(const StageBV2Args &a, hipStream_t stream);

@@ -580,6 +580,9 @@ __global__ __launch_bounds__(64 * NW) void stageb_v2(StageBV2Args a) {
     // fewer erasures than emax: its later chunks would stream every row for nothing)
     if (e <= 0 || a.j_base + static_cast<int>(blockIdx.y) * NW * 8 >= e) return;
     const bool active = j0 < e;
+    // this workgroup's input rows [i0, i0 + nr) (row slices; otherwise all e)
+    const int i0 = a.row_slice > 0 ? static_cast<int>(blockIdx.z) * a.row_slice : 0;
+    const int nr = a.row_slice > 0 ? max(0, min(e - i0, a.row_slice)) : e;
     const long long gbase = static_cast<long long>(g) * a.in_gstride;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.in + gbase), static_cast<short>(0), static_cast<int>(a.in_gstride), 0x00020000);
@@ -592,18 +595,18 @@ __global__ __launch_bounds__(64 * NW) void stageb_v2(StageBV2Args a) {
     };
     const uint32_t dsrc = piece_src(NW >= 2 ? wave : 0);
     const uint32_t dsrc1 = NW >= 2 ? 0u : piece_src(1);
-    const int elast = e - 1;
+    const int elast = i0 + max(nr, 1) - 1;
     auto issue = [&](int i) {
         if (wave < 2) {
-            const int x = min(i, elast);
+            const int x = min(i0 + i, elast);
             const uint32_t w = __builtin_amdgcn_readlane(rrv, x >> 2);
             const uint32_t soff = ((w >> (8 * (x & 3))) & 0xFFu) * static_cast<uint32_t>(geo.B);
             uint8_t *dst = ring + (i % RB_R) * RB_ROW + wave * 1024;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)dst, 16,
-                                                     i < e ? dsrc : 0x80000000u, soff, 0, 0);
+                                                     i < nr ? dsrc : 0x80000000u, soff, 0, 0);
             if (NW == 1)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(dst + 1024), 16,
-                                                         i < e ? dsrc1 : 0x80000000u, soff, 0, 0);
+                                                         i < nr ? dsrc1 : 0x80000000u, soff, 0, 0);
         }
     };
     u32x16 a01, a23, a45, a67;
@@ -617,7 +620,7 @@ __global__ __launch_bounds__(64 * NW) void stageb_v2(StageBV2Args a) {
         const int i = lane + 64 * u;
         if (i < 2 * e && active) cf[wave][i >> 1][i & 1] = cfw[u];
     }
-    const int ngroups = (e + RB_S - 1) / RB_S;
+    const int ngroups = (nr + RB_S - 1) / RB_S;
     for (int ig = 0; ig < ngroups; ++ig) {
         // own DMAs of rows RB_S*ig.. landed (RB_R - 2 * RB_S younger ones may be outstanding);
         // the first barrier also publishes the coefficient copies
@@ -631,13 +634,13 @@ __global__ __launch_bounds__(64 * NW) void stageb_v2(StageBV2Args a) {
 #pragma unroll
         for (int r = 0; r < RB_S; ++r) {
             const int i = ig * RB_S + r;
-            if (i >= e) break;  // uniform
+            if (i >= nr) break;  // uniform
             const uint8_t *slot = ring + (i % RB_R) * RB_ROW + lane * 4;
             Row8 d;
 #pragma unroll
             for (int s = 0; s < 8; ++s) d.w[s] = *reinterpret_cast<const uint32_t *>(slot + s * 256);
-            const uint32_t q0 = __builtin_amdgcn_readfirstlane(cf[wave][i][0]);
-            const uint32_t q1 = __builtin_amdgcn_readfirstlane(cf[wave][i][1]);
+            const uint32_t q0 = __builtin_amdgcn_readfirstlane(cf[wave][i0 + i][0]);
+            const uint32_t q1 = __builtin_amdgcn_readfirstlane(cf[wave][i0 + i][1]);
             v2_row(d, q0, q1, lo, hi, a01, a23, a45, a67, z0, z1);
         }
     }
@@ -651,7 +654,8 @@ __global__ __launch_bounds__(64 * NW) void stageb_v2(StageBV2Args a) {
         acc[4][b] = a45[b]; acc[5][b] = a45[8 + b];
         acc[6][b] = a67[b]; acc[7][b] = a67[8 + b];
     }
-    uint8_t *out = a.out + static_cast<long long>(g) * a.out_gstride + colx_off(c0 + lane, geo.nq, geo.sub);
+    uint8_t *out = a.out + static_cast<long long>(g) * a.out_gstride + colx_off(c0 + lane, geo.nq, geo.sub) +
+                   (a.row_slice > 0 ? static_cast<long long>(blockIdx.z) * a.out_slice_bytes : 0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         if (j0 + j >= e) break;
@@ -694,7 +698,8 @@ hipError_t launch_stageb_v2(const StageBV2Args &a, hipStream_t stream) {
     if (tail) --chunks;
     StageBV2Args m = a;
     m.j_base = 0;
-    dim3 grid(static_cast<unsigned>(ncc) * a.groups, chunks, 1);
+    const unsigned zs = a.row_slice > 0 ? static_cast<unsigned>(a.row_slices) : 1u;
+    dim3 grid(static_cast<unsigned>(ncc) * a.groups, chunks, zs);
     if (nw1 == 1)
         hipLaunchKernelGGL(stageb_v2<1>, grid, dim3(64), 0, stream, m);
     else if (nw1 == 2)
@@ -705,7 +710,7 @@ hipError_t launch_stageb_v2(const StageBV2Args &a, hipStream_t stream) {
         hipLaunchKernelGGL(stageb_v2<8>, grid, dim3(512), 0, stream, m);
     if (tail) {
         m.j_base = chunks * nw1 * 8;
-        dim3 tg(static_cast<unsigned>(ncc) * a.groups, 1, 1);
+        dim3 tg(static_cast<unsigned>(ncc) * a.groups, 1, zs);
         if (rem == 1)
             hipLaunchKernelGGL((stageb_v2<1, V2_MAXE>), tg, dim3(64), 0, stream, m);
         else

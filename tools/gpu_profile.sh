@@ -34,7 +34,7 @@ if [ -n "${IFETCH:-}" ]; then  # e.g. IFETCH="SQC_ICACHE_REQ SQC_ICACHE_MISSES" 
   python3 tools/pmc_summary.py "$OUT/ifetch" > "$OUT/ifetch.txt"
 fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run --output-format csv -- \
-  python3 bench.py --steps 10 --warmup 2 --no-cpu --host-calls 0 --no-sweep > "$OUT/bench.log" 2>&1 || { echo "stats run failed"; tail -5 "$OUT/bench.log"; exit 1; }
+  python3 bench.py --steps 40 --warmup 3 --no-cpu --host-calls 0 --no-sweep > "$OUT/bench.log" 2>&1 || { echo "stats run failed"; tail -5 "$OUT/bench.log"; exit 1; }
 cp "$(find "$OUT/stats" -name run_kernel_stats.csv | head -1)" "$OUT/bench_kernel_stats.csv"
 python3 tools/kstats.py "$OUT/stats" > "$OUT/kstats.txt"
 rm -rf "$OUT/fetch" "$OUT/write" "$OUT/sq" "$OUT/ifetch" "$OUT/stats"
