@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -56,6 +57,73 @@ int host_threads() {
     return n;
 }
 
+// Persistent host workers for the framing copies: host_threads() - 1 threads started on first use
+// and parked on a condition variable between calls (spawning and joining 15 threads per framing
+// pass cost ~0.3 ms each time, two passes per chunk). Never destroyed: parked threads are fine at
+// process exit.
+class Workers {
+  public:
+    explicit Workers(int n) : nthreads_(n) {
+        for (int w = 1; w < n; ++w) th_.emplace_back([this, w] { loop(w); });
+        for (auto &t : th_) t.detach();
+    }
+    int size() const { return nthreads_; }
+    // fn(i) for i in [0, n) split into t <= size() contiguous ranges; the caller runs range 0
+    void run(int n, int t, const std::function<void(int)> &fn) {
+        std::lock_guard<std::mutex> one(run_mu_);  // one pass at a time
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            fn_ = &fn;
+            n_ = n;
+            t_ = t;
+            pending_ = nthreads_ - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        range(0, n, t, fn);
+        std::unique_lock<std::mutex> g(mu_);
+        done_.wait(g, [this] { return pending_ == 0; });
+    }
+
+  private:
+    static void range(int w, int n, int t, const std::function<void(int)> &fn) {
+        if (w >= t) return;
+        const int a = static_cast<int>(static_cast<long long>(n) * w / t);
+        const int b = static_cast<int>(static_cast<long long>(n) * (w + 1) / t);
+        for (int i = a; i < b; ++i) fn(i);
+    }
+    void loop(int w) {
+        unsigned long long seen = 0;
+        for (;;) {
+            const std::function<void(int)> *fn;
+            int n, t;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return gen_ != seen; });
+                seen = gen_;
+                fn = fn_;
+                n = n_;
+                t = t_;
+            }
+            range(w, n, t, *fn);
+            std::lock_guard<std::mutex> g(mu_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    const int nthreads_;
+    std::vector<std::thread> th_;
+    std::mutex run_mu_, mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)> *fn_ = nullptr;
+    int n_ = 0, t_ = 0, pending_ = 0;
+    unsigned long long gen_ = 0;
+};
+
+Workers &workers() {
+    static Workers *w = new Workers(host_threads());
+    return *w;
+}
+
 // fn(i) for i in [0, n) on up to host_threads() threads (contiguous ranges).
 void parallel_for(int n, const std::function<void(int)> &fn) {
     const int t = std::min(host_threads(), std::max(1, n / 4));
@@ -63,16 +131,7 @@ void parallel_for(int n, const std::function<void(int)> &fn) {
         for (int i = 0; i < n; ++i) fn(i);
         return;
     }
-    std::vector<std::thread> th;
-    th.reserve(t - 1);
-    auto range = [&](int w) {
-        const int a = static_cast<int>(static_cast<long long>(n) * w / t);
-        const int b = static_cast<int>(static_cast<long long>(n) * (w + 1) / t);
-        for (int i = a; i < b; ++i) fn(i);
-    };
-    for (int w = 1; w < t; ++w) th.emplace_back(range, w);
-    range(0);
-    for (auto &x : th) x.join();
+    workers().run(n, t, fn);
 }
 
 // Two pinned + device staging slots on one stream; each slot remembers how to finish the chunk
