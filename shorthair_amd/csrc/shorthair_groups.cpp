@@ -460,7 +460,10 @@ extern "C" int shorthair_recover_groups(const ShorthairRxGroup *groups, int coun
                 SG_CHECK(hipMemcpy2DAsync(h + o_out, B, d + static_cast<size_t>(k - 1) * B, in_g, B, gn,
                                           hipMemcpyDeviceToHost, st.stream));
             }
-            if (!on_packet) return 0;  // decode only (no delivery)
+            if (!on_packet) {  // decode only (no delivery): still wait for the chunk before the
+                fin = [] {};   // slot is reused and before the call returns
+                return 0;
+            }
             fin = [&, g0, gn, h]() {
                 // RecoverGroup :741-756: deliver recovered blocks whose length prefix fits
                 for (int j = 0; j < gn; ++j) {
