@@ -5,7 +5,7 @@
 // (:764-902) keeps, for many groups per call.
 //
 // Layer above the public batch ABI (cauchy_256_batch.h): groups are bucketed by (k, m, B), a
-// bucket is cut into chunks of ~kChunkBytes of blocks, and chunks alternate between two pinned
+// bucket is cut into chunks of ~chunk_bytes() of blocks, and chunks alternate between two pinned
 // staging slots. For chunk i the host threads frame the blocks into slot i%2 while the GPU runs
 // chunk i-1 (H2D, kernel, D2H on one stream); once slot i%2's previous chunk has completed its
 // outputs are unframed on the host threads. So host framing, PCIe and kernels overlap, and the
@@ -29,7 +29,15 @@
 
 namespace {
 
-constexpr size_t kChunkBytes = size_t(48) << 20;  // device bytes per chunk (inputs + outputs)
+// device bytes per chunk (inputs + outputs); SH_PKT_CHUNK_MB: measurement switch
+size_t chunk_bytes() {
+    static const size_t b = [] {
+        const char *e = std::getenv("SH_PKT_CHUNK_MB");
+        const int mb = e ? std::atoi(e) : 48;
+        return static_cast<size_t>(std::max(1, mb)) << 20;
+    }();
+    return b;
+}
 
 #define SG_CHECK(expr)                                                                        \
     do {                                                                                      \
@@ -286,7 +294,7 @@ extern "C" int shorthair_encode_groups(ShorthairTxGroup *groups, int count) {
         const int k = std::get<0>(kv.first), m = std::get<1>(kv.first), B = std::get<2>(kv.first);
         const std::vector<int> &ids = kv.second;
         const size_t in_g = static_cast<size_t>(k) * B, out_g = static_cast<size_t>(m) * B;
-        const int per = static_cast<int>(std::max<size_t>(1, kChunkBytes / (in_g + out_g)));
+        const int per = static_cast<int>(std::max<size_t>(1, chunk_bytes() / (in_g + out_g)));
         const int n = static_cast<int>(ids.size());
         const int chunks = (n + per - 1) / per;
         const size_t slot_bytes = static_cast<size_t>(std::min(per, n)) * (in_g + out_g);
@@ -408,7 +416,7 @@ extern "C" int shorthair_recover_groups(const ShorthairRxGroup *groups, int coun
         const size_t in_g = static_cast<size_t>(k) * B;
         const size_t out_g = m >= 2 ? static_cast<size_t>(emax) * B : static_cast<size_t>(B);
         const size_t per_g = in_g + k + out_g + emax + 4;
-        const int per = static_cast<int>(std::max<size_t>(1, kChunkBytes / per_g));
+        const int per = static_cast<int>(std::max<size_t>(1, chunk_bytes() / per_g));
         const int n = static_cast<int>(ids.size());
         const int chunks = (n + per - 1) / per;
         const int cap = std::min(per, n);
