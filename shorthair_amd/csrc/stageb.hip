@@ -735,7 +735,8 @@ bool stageb_small_ok(const Geometry &geo, int emax) {
 __global__ __launch_bounds__(64) void stageb_small(StageBSmallArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t tab[32 * 64];  // 8 KB window tables [entry][lane]
     __shared__ __attribute__((aligned(16))) uint32_t rbt[256 * 4];  // entry bytes of c * 2^b, b = 0..7
-    __shared__ uint8_t rrs[16][128];                                // row lists of the wave's groups
+    extern __shared__ uint8_t rrs[];  // row lists of the wave's groups, [gpw][emax] (launch-sized:
+                                      // 2 KB fixed kept 11 workgroups per CU instead of 13)
     const Geometry geo = a.geo;
     const int lane = threadIdx.x;
     const int gpw = 64 / geo.nq;
@@ -758,7 +759,7 @@ __global__ __launch_bounds__(64) void stageb_small(StageBSmallArgs a) {
     for (int t = lane; t < gpw * a.emax; t += 64) {
         const int sl = t / a.emax, i = t - sl * a.emax;
         const int gg = g0 + sl;
-        rrs[sl][i] = (gg < a.groups && i < a.e[gg]) ? a.rrow[static_cast<long long>(gg) * a.ldR + i] : 0;
+        rrs[sl * a.emax + i] = (gg < a.groups && i < a.e[gg]) ? a.rrow[static_cast<long long>(gg) * a.ldR + i] : 0;
     }
     __syncthreads();
     const int el = valid ? max(a.e[g], 0) : 0;
@@ -774,7 +775,7 @@ __global__ __launch_bounds__(64) void stageb_small(StageBSmallArgs a) {
     auto load = [&](int i, uint32_t (&d)[8], uint64_t &cc) {
         // lanes past the wave's last group (gs >= gpw, or past the batch) read row 0 of group g0:
         // their rrs row was never written, and any other row could lie past the workspace
-        const int r = valid ? rrs[gs][min(i, max(el - 1, 0))] : 0;
+        const int r = valid ? rrs[gs * a.emax + min(i, max(el - 1, 0))] : 0;
         const uint8_t *p = res + static_cast<long long>(r) * geo.B;
 #pragma unroll
         for (int s = 0; s < 8; ++s) __builtin_memcpy(&d[s], p + s * geo.sub, 4);
@@ -838,7 +839,8 @@ hipError_t launch_stageb_small(const StageBSmallArgs &a, hipStream_t stream) {
     if (!stageb_small_ok(a.geo, a.emax)) return hipErrorNotSupported;
     const int gpw = 64 / a.geo.nq;
     dim3 grid(static_cast<unsigned>((a.groups + gpw - 1) / gpw), (a.emax + 7) / 8, 1);
-    hipLaunchKernelGGL(stageb_small, grid, dim3(64), 0, stream, a);
+    const size_t rrs_bytes = (static_cast<size_t>(gpw) * a.emax + 15) & ~static_cast<size_t>(15);
+    hipLaunchKernelGGL(stageb_small, grid, dim3(64), rrs_bytes, stream, a);
     return hipGetLastError();
 }
 
