@@ -11,6 +11,7 @@
 // outputs are unframed on the host threads. So host framing, PCIe and kernels overlap, and the
 // only host work per byte is the framing copy the reference also does (its memset/memcpy).
 #include <hip/hip_runtime.h>
+#include <emmintrin.h>
 
 #include <algorithm>
 #include <condition_variable>
@@ -55,6 +56,28 @@ inline void put_u16(uint8_t *p, unsigned v) {  // WriteU16_LE (ShorthairDetails.
     p[1] = static_cast<uint8_t>(v >> 8);
 }
 inline unsigned get_u16(const uint8_t *p) { return p[0] | (static_cast<unsigned>(p[1]) << 8); }
+
+// Framing copy into the pinned staging buffer: 16-byte non-temporal stores for the aligned body
+// (the staging bytes are read next by the H2D DMA, not by this core, so a cached store's
+// read-for-ownership of every line is wasted memory traffic), plain copies for the ragged ends.
+// Callers fence (framing_fence) before the buffer is handed to the DMA.
+inline void framing_copy(uint8_t *dst, const uint8_t *src, size_t n) {
+    if (n < 64) {
+        std::memcpy(dst, src, n);
+        return;
+    }
+    const size_t head = (16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15;
+    std::memcpy(dst, src, head);
+    dst += head;
+    src += head;
+    n -= head;
+    const size_t body = n & ~static_cast<size_t>(15);
+    for (size_t i = 0; i < body; i += 16)
+        _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i),
+                         _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i)));
+    std::memcpy(dst + body, src + body, n - body);
+}
+inline void framing_fence() { _mm_sfence(); }
 
 int host_threads() {
     static const int n = [] {
@@ -308,9 +331,10 @@ extern "C" int shorthair_encode_groups(ShorthairTxGroup *groups, int count) {
                 for (int x = 0; x < k; ++x, blk += B) {
                     const int len = g.lens[x];
                     put_u16(blk, len);
-                    std::memcpy(blk + 2, g.packets[x], len);
+                    framing_copy(blk + 2, static_cast<const uint8_t *>(g.packets[x]), len);
                     std::memset(blk + 2 + len, 0, B - 2 - len);
                 }
+                framing_fence();
             });
         };
         auto submit = [&](int c, Slot &s, std::function<void()> &fin) -> int {
@@ -437,14 +461,15 @@ extern "C" int shorthair_recover_groups(const ShorthairRxGroup *groups, int coun
                 for (int i = 0; i < g.n_orig; ++i, ++x, blk += B) {
                     const int len = g.orig_lens[i];
                     put_u16(blk, len);
-                    std::memcpy(blk + 2, g.orig_data[i], len);
+                    framing_copy(blk + 2, static_cast<const uint8_t *>(g.orig_data[i]), len);
                     std::memset(blk + 2 + len, 0, B - 2 - len);
                     rows[x] = g.orig_ids[i];
                 }
                 for (int i = 0; i < r.use; ++i, ++x, blk += B) {  // :727-735
-                    std::memcpy(blk, g.rec_packets[i] + 3, B);
+                    framing_copy(blk, g.rec_packets[i] + 3, B);
                     rows[x] = g.rec_packets[i][0];
                 }
+                framing_fence();
             });
         };
         auto submit = [&](int c, Slot &s, std::function<void()> &fin) -> int {
