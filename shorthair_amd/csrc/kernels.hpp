@@ -149,6 +149,7 @@ struct StageBSmallArgs {
     int emax;
     int groups;
     Geometry geo;
+    int xcd_map;              // set by the launcher: 1 = XCD-aware block order (see stageb_small)
 };
 bool stageb_small_ok(const Geometry &geo, int emax);
 hipError_t launch_stageb_small(const StageBSmallArgs &a, hipStream_t stream);

@@ -741,10 +741,22 @@ __global__ __launch_bounds__(64) void stageb_small(StageBSmallArgs a) {
     const int lane = threadIdx.x;
     const int gpw = 64 / geo.nq;
     const int gs = lane / geo.nq, q = lane - gs * geo.nq;
-    const int g0 = blockIdx.x * gpw;
+    // Block order: every output chunk of a group block streams the same e residual rows, so the
+    // chunks of one group block are dealt to one XCD back to back (block b -> XCD b % 8) and the
+    // later ones read the rows from that XCD's L2; in chunk-major order ((224,32,256): 4 chunks)
+    // each chunk fetched them from memory again (4.5x the rows' bytes, PMC).
+    int gb = blockIdx.x, chunk = blockIdx.y;
+    if (a.xcd_map) {
+        const int nch = (a.emax + 7) / 8;
+        const int i = static_cast<int>(blockIdx.x) >> 3;
+        chunk = i % nch;
+        gb = (i / nch) * 8 + (static_cast<int>(blockIdx.x) & 7);
+        if (gb * gpw >= a.groups) return;  // padding blocks of the last XCD round
+    }
+    const int g0 = gb * gpw;
     const bool valid = gs < gpw && g0 + gs < a.groups;
     const int g = valid ? g0 + gs : g0;
-    const int j0 = blockIdx.y * 8;
+    const int j0 = chunk * 8;
     for (int c = lane; c < 256; c += 64) {
         uint32_t w[4] = {0, 0, 0, 0};
         uint32_t v = static_cast<uint32_t>(c);
@@ -838,9 +850,14 @@ hipError_t launch_stageb_small(const StageBSmallArgs &a, hipStream_t stream) {
     if (a.groups <= 0 || a.emax <= 0) return hipSuccess;
     if (!stageb_small_ok(a.geo, a.emax)) return hipErrorNotSupported;
     const int gpw = 64 / a.geo.nq;
-    dim3 grid(static_cast<unsigned>((a.groups + gpw - 1) / gpw), (a.emax + 7) / 8, 1);
+    const int ngb = (a.groups + gpw - 1) / gpw, nch = (a.emax + 7) / 8;
+    static const bool xcd = !std::getenv("SH_SMALL_XCD") || std::atoi(std::getenv("SH_SMALL_XCD")) != 0;  // measurement
+    StageBSmallArgs m = a;
+    m.xcd_map = xcd && nch > 1 ? 1 : 0;
+    const dim3 grid = m.xcd_map ? dim3(static_cast<unsigned>(8 * nch * ((ngb + 7) / 8)), 1, 1)
+                                : dim3(static_cast<unsigned>(ngb), static_cast<unsigned>(nch), 1);
     const size_t rrs_bytes = (static_cast<size_t>(gpw) * a.emax + 15) & ~static_cast<size_t>(15);
-    hipLaunchKernelGGL(stageb_small, grid, dim3(64), rrs_bytes, stream, a);
+    hipLaunchKernelGGL(stageb_small, grid, dim3(64), rrs_bytes, stream, m);
     return hipGetLastError();
 }
 
