@@ -50,6 +50,10 @@ def _stale():
 
 FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result"]
 FLAGS += os.environ.get("SH_EXTRA_FLAGS", "").split()  # experiments only (tools/build_variant.sh)
+# A/B variants only (tools/build_variant.sh): the environment switches of csrc/measure.hpp. The
+# product library is never built with it.
+if os.environ.get("SH_MEASUREMENT") == "1":
+    FLAGS.append("-DSH_MEASUREMENT_BUILD")
 OBJ_DIR = os.path.join(HERE, os.environ.get("SH_OBJ_DIR", "build_obj"))
 
 

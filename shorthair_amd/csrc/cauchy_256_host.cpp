@@ -25,6 +25,7 @@
 #include "cauchy_math.hpp"
 #include "colsnip.h"
 #include "kernels.hpp"
+#include "measure.hpp"
 
 namespace {
 
@@ -89,10 +90,6 @@ struct StreamState {
     std::mutex mu;
     DevBuf ws;
     int *d_errors = nullptr;
-    // chunk-pipelined decode (decode_core): stage B of chunk j on `side` beside stage A of chunk
-    // j + 1 on the calling stream, joined by `evs` (created on first use, guarded by mu)
-    hipStream_t side = nullptr;
-    std::vector<hipEvent_t> evs;
 };
 
 // One launch of the tile kernels: output rows [row0, row0 + nrows) with its snippet-address table.
@@ -283,7 +280,7 @@ uint8_t *generator(Context &c, int k, int m) {
 // addresses from their low dwords).
 bool tile_usable(Context &c, int k, int m, int B) {
     if (k < 2 || m < 2 || k + m > 256 || !sh::tile_ok(B)) return false;
-    if (std::getenv("SH_NO_TILE")) return false;  // measurement switch: the older generic kernels
+    if (SH_MEASURE_ENV("SH_NO_TILE")) return false;  // measurement switch: the older generic kernels
     const uint64_t lo = c.snip_base, hi = c.snip_base + static_cast<uint64_t>(sh::SNIP_NULL + 1) * sh::SNIP_STRIDE;
     return (lo >> 32) == (hi >> 32);
 }
@@ -291,7 +288,7 @@ bool tile_usable(Context &c, int k, int m, int B) {
 // Measurement switch (never the default): SH_FORCE_TILE=1 routes shapes that have compile-time
 // kernels through the tile kernels too, to compare the two on the same shape.
 bool force_tile() {
-    static const bool f = std::getenv("SH_FORCE_TILE") != nullptr;
+    static const bool f = SH_MEASURE_ENV("SH_FORCE_TILE") != nullptr;
     return f;
 }
 
@@ -313,8 +310,8 @@ const std::vector<TileLaunch> *tile_plan(Context &c, int k, int m, bool dec) {
     // ((180,76) 2.30 vs 2.43 ms; the others within 5 %): a column snippet's table (16 KB per
     // generator row) misses the instruction cache where the 18 KB per-row table stays resident.
     // SH_NO_COL / SH_COL_ENC: measurement switches.
-    static const bool no_col = std::getenv("SH_NO_COL") != nullptr;
-    static const bool col_enc = std::getenv("SH_COL_ENC") != nullptr;
+    static const bool no_col = SH_MEASURE_ENV("SH_NO_COL") != nullptr;
+    static const bool col_enc = SH_MEASURE_ENV("SH_COL_ENC") != nullptr;
     const bool col = m >= 7 && c.col_ok && !no_col && (dec || col_enc);
     std::vector<uint8_t> xp, yp;
     if (col) sh::cauchy_params(k, m, xp, yp);
@@ -408,8 +405,8 @@ int latency_slices(int nsteps) {
     // SH_SLICE_MAX / SH_SLICE_STEPS: measurement switches (slices at most, steps per slice at least)
     // (200,32,1400) single-group calls: 8 x 25 steps 80 / 112 us (encode / decode), 16 x 12 74 / 104,
     // 32 x 6 70 / 104 (profiles/r05/ab_runs.txt block 13)
-    static const int mx = std::getenv("SH_SLICE_MAX") ? std::atoi(std::getenv("SH_SLICE_MAX")) : 32;
-    static const int st = std::getenv("SH_SLICE_STEPS") ? std::atoi(std::getenv("SH_SLICE_STEPS")) : 6;
+    static const int mx = sh::measure_int(SH_MEASURE_ENV("SH_SLICE_MAX"), 32);
+    static const int st = sh::measure_int(SH_MEASURE_ENV("SH_SLICE_STEPS"), 6);
     return std::max(1, std::min(std::min(mx, kSliceCap), nsteps / std::max(st, 1)));
 }
 
@@ -538,9 +535,9 @@ struct DecodeWS {
 // SH_STAGEB_OLD=1 (measurement switch) selects round 2's kernels everywhere; SH_V2_MIN / SH_V2_MAX
 // bound the emax served by stageb_v2.
 bool stageb_v2_on(const sh::Geometry &geo, int emax) {
-    static const bool old = std::getenv("SH_STAGEB_OLD") != nullptr;
-    static const int vmax = std::getenv("SH_V2_MAX") ? std::atoi(std::getenv("SH_V2_MAX")) : 128;  // measurement
-    static const int vmin = std::getenv("SH_V2_MIN") ? std::atoi(std::getenv("SH_V2_MIN")) : 8;    // measurement
+    static const bool old = SH_MEASURE_ENV("SH_STAGEB_OLD") != nullptr;
+    static const int vmax = sh::measure_int(SH_MEASURE_ENV("SH_V2_MAX"), 128);  // measurement
+    static const int vmin = sh::measure_int(SH_MEASURE_ENV("SH_V2_MIN"), 8);    // measurement
     return !old && emax > vmin && emax <= vmax && sh::stageb_v2_ok(geo, emax);
 }
 
@@ -582,7 +579,7 @@ size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool n
 // Rows per stage-B slice on the single-group latency path (SH_SB_SLICE, measurement switch; 0 = one
 // workgroup streams all e rows).
 int stageb_row_slice() {
-    static const int n = std::getenv("SH_SB_SLICE") ? std::atoi(std::getenv("SH_SB_SLICE")) : 8;
+    static const int n = sh::measure_int(SH_MEASURE_ENV("SH_SB_SLICE"), 8);
     return std::max(0, n);
 }
 
@@ -623,7 +620,10 @@ hipError_t launch_stage_b(const DecodeWS &w, int n_in, int B, int groups, uint8_
         f.groups = groups;
         f.geo = sh::fixed_geometry(B);
         f.snip_base = ctx().snip_base;
-        const int rs = stageb_row_slice();
+        // at most kSliceCap partial outputs fit slice_scratch (a small measurement
+        // setting of SH_SB_SLICE must not write past it)
+        const int rs0 = stageb_row_slice();
+        const int rs = rs0 > 0 ? std::max(rs0, (w.emax + kSliceCap - 1) / kSliceCap) : 0;
         if (slice_scratch && groups == 1 && rs > 0 && w.emax > rs) {
             f.row_slice = rs;
             f.row_slices = (w.emax + rs - 1) / rs;
@@ -663,12 +663,6 @@ hipError_t launch_stage_b(const DecodeWS &w, int n_in, int B, int groups, uint8_
     b.groups = groups;
     b.geo = sh::make_geometry(B);
     return sh::launch_stageb(b, w.emax, s);
-}
-
-// Chunks of the pipelined decode (SH_DEC_CHUNKS, measurement switch; 1 = one launch per stage)
-int dec_chunks(int groups) {
-    static const int n = std::getenv("SH_DEC_CHUNKS") ? std::atoi(std::getenv("SH_DEC_CHUNKS")) : 1;
-    return (n > 1 && groups >= 256 * n) ? n : 1;
 }
 
 // Common decode core (m >= 2, valid params): writes recovered blocks densely into `dst`
@@ -721,42 +715,6 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
     if (ev) SH_CHECK(hipEventRecord(ev[1], s));
 
     const Geometry geo = sh::make_geometry(B);
-    const int nch = dec_chunks(groups);
-    if (w.fixed && w.v2 && nch > 1 && !slice_scratch && sh::has_fixed(k, m, B) && !force_tile()) {
-        // Chunk-pipelined (measurement switch SH_DEC_CHUNKS): stage A of chunk j on `s`, stage B
-        // of chunk j on a side stream once that stage A is done, so stage B (snippet calls: SALU
-        // and latency) runs beside the next chunk's stage A (VALU and memory).
-        StreamState *ss = stream_state(c, s);
-        if (!ss) return -2;
-        if (!ss->side) SH_CHECK(hipStreamCreateWithFlags(&ss->side, hipStreamNonBlocking));
-        while (static_cast<int>(ss->evs.size()) < nch + 1) {
-            hipEvent_t e;
-            SH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            ss->evs.push_back(e);
-        }
-        for (int j = 0; j < nch; ++j) {
-            const int lo = static_cast<int>(static_cast<long long>(groups) * j / nch);
-            const int n = static_cast<int>(static_cast<long long>(groups) * (j + 1) / nch) - lo;
-            SH_CHECK(launch_fixed_batch(k, m, B, n, d_blocks + static_cast<size_t>(lo) * k * B,
-                                        static_cast<long long>(k) * B,
-                                        w.residual + static_cast<size_t>(lo) * m * B, static_cast<long long>(m) * B,
-                                        w.pos + static_cast<size_t>(lo) * round4(k),
-                                        w.rpos + static_cast<size_t>(lo) * round4(m), true, s));
-            SH_CHECK(hipEventRecord(ss->evs[j], s));
-            SH_CHECK(hipStreamWaitEvent(ss->side, ss->evs[j], 0));
-            DecodeWS v = w;
-            v.e += lo;
-            v.rrow += static_cast<size_t>(lo) * round4(w.emax);
-            v.coefB += static_cast<size_t>(lo) * w.coefB_gs;
-            v.residual += static_cast<size_t>(lo) * m * B;
-            SH_CHECK(launch_stage_b(v, m, B, n, dst + static_cast<size_t>(lo) * w.emax * B, ss->side));
-        }
-        if (ev) SH_CHECK(hipEventRecord(ev[2], s));
-        SH_CHECK(hipEventRecord(ss->evs[nch], ss->side));
-        SH_CHECK(hipStreamWaitEvent(s, ss->evs[nch], 0));
-        if (ev) SH_CHECK(hipEventRecord(ev[3], s));
-        return 0;
-    }
     if (w.fixed) {
         // Stage A (compile-time generator, all m rows, erased columns read as zeros):
         //   residual_y = R_y + sum_{received x} M(C[y][x]) d_x
@@ -1061,7 +1019,7 @@ extern "C" int cauchy_256_batch_path(int k, int m, int block_bytes) {
     // initialises the GPU): the snippet table's one-4-GB-page condition needs the loaded code
     // object and is checked at launch (generic kernels otherwise); once the library is
     // initialised the answer includes it.
-    if (k < 2 || m < 2 || !sh::tile_ok(block_bytes) || std::getenv("SH_NO_TILE")) return 0;
+    if (k < 2 || m < 2 || !sh::tile_ok(block_bytes) || SH_MEASURE_ENV("SH_NO_TILE")) return 0;
     Context &c = ctx();
     std::lock_guard<std::mutex> g(c.mu);
     return !c.ready || tile_usable(c, k, m, block_bytes) ? 2 : 0;
@@ -1212,7 +1170,10 @@ extern "C" int cauchy_256_encode(int k, int m, const unsigned char *data_ptrs[],
     for (int x = 0; x < kin; ++x) std::memcpy(h + static_cast<size_t>(x) * block_bytes, data_ptrs[x], block_bytes);
     SH_CHECK(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, st.stream));
     const int rc = encode_batch(k, m, block_bytes, 1, d, d + in_bytes, st.stream, d + in_bytes + out_bytes);
-    if (rc == -2) return rc;
+    if (rc == -2) {
+        (void)hipStreamSynchronize(st.stream);  // the slot is released on return
+        return rc;
+    }
     // Like the reference, a rejected call has still written recovery row 0.
     const size_t copy = (rc == 0) ? out_bytes : static_cast<size_t>(block_bytes);
     SH_CHECK(hipMemcpyAsync(h + in_bytes, d + in_bytes, copy, hipMemcpyDeviceToHost, st.stream));
@@ -1276,7 +1237,11 @@ extern "C" int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes) {
         SH_CHECK(hipMemcpyAsync(d, h, up, hipMemcpyHostToDevice, st.stream));
         const int rc = decode_batch(k, m, block_bytes, 1, d, d + data_bytes, st.stream, nullptr,
                                     d + ws_off + ws_bytes, h, e, d + ws_off, hs);
-        if (rc != 0) return rc;
+        if (rc != 0) {
+            // the staging slot is released on return: nothing queued may still read it
+            (void)hipStreamSynchronize(st.stream);
+            return rc;
+        }
         SH_CHECK(hipStreamSynchronize(st.stream));
         for (int l = 0; l < e; ++l) {
             std::memcpy(blocks[rec[l]].data, h + static_cast<size_t>(l) * block_bytes, block_bytes);
@@ -1289,7 +1254,10 @@ extern "C" int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes) {
     int *e_host = reinterpret_cast<int *>(h + ((data_bytes + k + 3) & ~static_cast<size_t>(3)));
     *e_host = 0;
     const int rc = decode_batch(k, m, block_bytes, 1, d, d + data_bytes, st.stream, e_host, d + data_bytes + 256);
-    if (rc != 0) return rc;
+    if (rc != 0) {
+        (void)hipStreamSynchronize(st.stream);
+        return rc;
+    }
     SH_CHECK(hipMemcpyAsync(h, d, data_bytes + k, hipMemcpyDeviceToHost, st.stream));
     SH_CHECK(hipStreamSynchronize(st.stream));
     if (*e_host < 0) return -1;

@@ -97,11 +97,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wg_rsrc(const uint8_t *base, l
 
 // Compile-time shape of one kernel instance.
 // DMA_ = false only in measurement builds (tools/gen_fixed_kernels.py SH_GEN_ABLATE=nodma).
-template <int K_, int M_, int P_, int CW_, int R_, bool DMA_ = true>
+// PW_ = parts per workgroup (default all P): with PW < P the P parts of a tile run in H = P / PW
+// workgroups, each reading the whole tile through its own ring (generator switch SH_PW, A/B
+// builds: fewer code streams per workgroup for H times the input reads).
+template <int K_, int M_, int P_, int CW_, int R_, bool DMA_ = true, int PW_ = P_>
 struct Shape {
     static constexpr int K = K_, M = M_, P = P_, CW = CW_, R = R_, W = 16;
+    static constexpr int PW = PW_, H = P_ / PW_;
+    static_assert(PW_ >= 1 && P_ % PW_ == 0, "parts per workgroup");
     static constexpr bool DMA = DMA_;
-    static constexpr int NW = CW * P, NT = 64 * NW, COLS = CW * 64;
+    static constexpr int NW = CW * PW, NT = 64 * NW, COLS = CW * 64;
     static constexpr int ROWB = COLS * 4;               // bytes of one sub-block row of a slot
     static constexpr int IMG = 8 * ROWB;                // bytes of one epilogue row image
     static constexpr int SLOT = IMG;                    // bytes per ring slot (one input block)
@@ -137,7 +142,7 @@ __device__ __forceinline__ WGInfo tile_info(int nq, long long col0, long long lo
     WGInfo w;
     w.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     w.lane = threadIdx.x & 63;
-    const int cw = w.wave / S::P;
+    const int cw = w.wave / S::PW;
     w.c = cw * 64 + w.lane;
     w.col0 = col0;
     w.lo = lo;
@@ -488,7 +493,7 @@ struct StreamSrc {
 // stored 8 runs of <= 176 bytes per instruction: the encode kernel was 3 % slower with it.) Row images are double-buffered by row parity: a wave
 // reads row y's image before it joins row y+1's barrier, so row y+2 may overwrite it.
 // Every wave of the workgroup joins one barrier per row of the largest part (pad() for the
-// shorter parts). The images ([2][P][SLOT] bytes) alias the ring (after Src::release()).
+// shorter parts). The images ([2][PW][SLOT] bytes) alias the ring (after Src::release()).
 template <class S>
 struct RowSink {
     __amdgpu_buffer_rsrc_t rsrc;
@@ -509,7 +514,7 @@ struct RowSink {
                                          int img_slot = 0) {
         rsrc = wg_rsrc(a.out, a.out_bytes, a.out_gstride, w.g_first);
         B = a.geo.B;
-        img = lds + img_slot * S::SLOT + part * S::IMG;
+        img = lds + img_slot * S::SLOT + (part % S::PW) * S::IMG;
         col0 = w.col0;
         lo = w.lo;
         hi = w.hi;
@@ -521,7 +526,7 @@ struct RowSink {
     // Per-lane piece offsets of the tile (called right before the first row).
     __device__ __forceinline__ void prepare() const {
         const int lane = threadIdx.x & 63;
-        const int cw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) / S::P;
+        const int cw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) / S::PW;
         wofs = static_cast<uint32_t>(cw * 64 + lane) * 4u;
         const long long cs = col0 > lo ? col0 : lo;
         const long long ce = col0 + S::COLS < hi ? col0 + S::COLS : hi;
@@ -570,7 +575,7 @@ struct RowSink {
     }
     template <int YI>
     __device__ __forceinline__ void row(int y, const uint32_t (&w)[8]) const {
-        uint8_t *im = img + (YI & 1) * S::P * S::IMG;
+        uint8_t *im = img + (YI & 1) * S::PW * S::IMG;
 #pragma unroll
         for (int b = 0; b < 8; ++b) *reinterpret_cast<uint32_t *>(im + b * S::ROWB + wofs) = w[b];
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -593,13 +598,13 @@ struct RowSink {
 template <class S, bool DEC, class SrcT, class SinkT>
 __device__ __forceinline__ int kernel_prologue(const FixedArgs &a, uint8_t *lds, SrcT &src,
                                                SinkT &sink, long long col0, long long lo, long long hi,
-                                               int img_slot = 0) {
+                                               int img_slot = 0, int hgrp = 0) {
     const WGInfo w = tile_info<S>(a.geo.nq, col0, lo, hi);
-    const int part = w.wave % S::P;
+    const int part = hgrp * S::PW + w.wave % S::PW;
     const int nq = a.geo.nq;
     // The row images of the epilogue alias the start of the ring: they are used only after the
     // last step, behind Src::release()'s barrier, so the ring gets that LDS as extra slots.
-    uint8_t *lds_pos = lds + (SrcT::kStream ? 2 * S::P * S::SLOT : S::R * S::SLOT);
+    uint8_t *lds_pos = lds + (SrcT::kStream ? 2 * S::PW * S::SLOT : S::R * S::SLOT);
     if (DEC) {
         const int ng = a.groups_per_wg;
         const int ghi = static_cast<int>(hi / nq);
@@ -671,6 +676,24 @@ __device__ __forceinline__ int xcd_tile(int b, int n) {
         }                                                                                         \
     } while (0)
 
+// Tile and part-group of a workgroup when a tile's parts run in H > 1 workgroups (Shape::PW < P):
+// the H workgroups of a tile get blocks 8 * (H * j + h) + x, i.e. the same XCD x and consecutive
+// dispatch slots there, so the second to H-th reads of the tile's input hit that XCD's L2. The
+// grid is rounded up to a multiple of 8 * H; a block past the last tile returns -1.
+template <class S>
+__device__ __forceinline__ int tile_of(const FixedArgs &a, int &hgrp) {
+    const long long cols = static_cast<long long>(a.groups) * a.geo.nq;
+    const int ntiles = static_cast<int>((cols + S::COLS - 1) / S::COLS);
+    if (S::H == 1) {
+        hgrp = 0;
+        return xcd_tile(blockIdx.x, gridDim.x);
+    }
+    const int x = blockIdx.x & 7, i = blockIdx.x >> 3;
+    hgrp = i % S::H;
+    const int vb = (i / S::H) * 8 + x;
+    return vb < ntiles ? xcd_tile(vb, ntiles) : -1;
+}
+
 inline int persistent_slots() {
     static const int cus = [] {
         int d = 0, n = 0;
@@ -691,12 +714,13 @@ inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArg
     constexpr bool dec = DEC;
     a.groups_per_wg = (S::COLS - 1) / a.geo.nq + 2;
     // ring (the row images of the epilogue alias it); a streaming source needs only the images
-    constexpr size_t front = STREAM ? 2ull * S::P * S::SLOT : static_cast<size_t>(S::R) * S::SLOT;
-    static_assert(STREAM || 2 * S::P * S::IMG <= S::R * S::SLOT, "row images must fit inside the ring");
+    constexpr size_t front = STREAM ? 2ull * S::PW * S::SLOT : static_cast<size_t>(S::R) * S::SLOT;
+    static_assert(STREAM || 2 * S::PW * S::IMG <= S::R * S::SLOT, "row images must fit inside the ring");
     // (+4: Src::pre4 reads up to 3 bytes past the last group's table)
     const size_t lds = front + (dec ? static_cast<size_t>(a.groups_per_wg) * (S::KP + S::MP) + 4 : 0);
     const long long cols = static_cast<long long>(a.groups) * a.geo.nq;
     unsigned blocks = static_cast<unsigned>((cols + S::COLS - 1) / S::COLS);  // one tile each
+    if (S::H > 1) blocks = (blocks + 7) / 8 * 8 * S::H;  // tile_of(): H part-groups per tile
     if (PERS) blocks = std::min<unsigned>(blocks, static_cast<unsigned>(persistent_slots()));
     if (tag) {
         bool used = false;
@@ -713,22 +737,25 @@ inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArg
 // One kernel + launcher of a generated (k, m): MODE enc (DEC = false) or dec (DEC = true);
 // MINW = waves per SIMD the registers are allocated for. The host routes shapes with
 // nq % 4 != 0 (a 16-byte chunk could straddle two groups) or sub < 16 to the generic kernel.
-#define FIXED_KERNEL(NAME, K, M, P, CW, R, MINW, MODE, DEC, DMA, STREAM)                          \
+#define FIXED_KERNEL(NAME, K, M, P, CW, R, MINW, MODE, DEC, DMA, STREAM, PW)                      \
     namespace sh {                                                                                \
     namespace fixed {                                                                             \
-    __global__ __launch_bounds__(64 * CW * P, MINW) void kern_##NAME##_##MODE(FixedArgs a) {      \
+    __global__ __launch_bounds__(64 * CW * PW, MINW) void kern_##NAME##_##MODE(FixedArgs a) {     \
         extern __shared__ __attribute__((aligned(16))) uint8_t lds[];                             \
-        using S = Shape<K, M, P, CW, R, DMA>;                                                     \
+        using S = Shape<K, M, P, CW, R, DMA, PW>;                                                 \
         using SrcT = typename std::conditional<STREAM, StreamSrc<S, DEC>, Src<S, DEC>>::type;     \
         SrcT src;                                                                                 \
         RowSink<S> sink;                                                                          \
-        const long long c0 = static_cast<long long>(xcd_tile(blockIdx.x, gridDim.x)) * S::COLS;  \
+        int hgrp;                                                                                 \
+        const int tile = tile_of<S>(a, hgrp);                                                     \
+        if (tile < 0) return;                                                                     \
+        const long long c0 = static_cast<long long>(tile) * S::COLS;                              \
         const int part = kernel_prologue<S, DEC>(a, lds, src, sink, c0, 0,                       \
-                                                 static_cast<long long>(a.groups) * a.geo.nq);   \
+                                                 static_cast<long long>(a.groups) * a.geo.nq, 0, hgrp); \
         run_##NAME##_##MODE(part, src, sink);                                                     \
     }                                                                                             \
     hipError_t launch_##NAME##_##MODE(FixedArgs a, hipStream_t s) {                               \
-        return launch_shape<Shape<K, M, P, CW, R, DMA>, DEC, STREAM>(a, s, kern_##NAME##_##MODE, #NAME "_" #MODE); \
+        return launch_shape<Shape<K, M, P, CW, R, DMA, PW>, DEC, STREAM>(a, s, kern_##NAME##_##MODE, #NAME "_" #MODE); \
     }                                                                                             \
     }                                                                                             \
     }

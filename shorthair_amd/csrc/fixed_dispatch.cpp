@@ -9,6 +9,7 @@
 
 #include "fixed_configs.h"  // from the generated-kernel directory (-I, see build.py)
 #include "kernels.hpp"
+#include "measure.hpp"
 
 namespace sh {
 namespace fixed {
@@ -18,13 +19,15 @@ namespace fixed {
 SH_FIXED_CONFIGS(SH_DECL)
 #undef SH_DECL
 
-// Measurement builds: SH_HSACO_DIR=<dir> makes every compile-time kernel whose code object
-// <dir>/<tag>.hsaco exists (tag = k<k>_m<m>_<enc|dec>, e.g. a tools/il_reorder.py layout of the
-// same kernel) launch from that code object. Not used by the product (the variable is unset).
+// Measurement builds only (-DSH_MEASUREMENT_BUILD, tools/build_variant.sh): SH_HSACO_DIR=<dir>
+// makes every compile-time kernel whose code object <dir>/<tag>.hsaco exists (tag =
+// k<k>_m<m>_<enc|dec>, e.g. a tools/il_reorder.py layout of the same kernel) launch from that code
+// object. The product library has neither the switch nor a module loader (measure.hpp).
 hipError_t module_launch(const char *tag, const FixedArgs &a, unsigned blocks, unsigned threads, size_t lds,
                          hipStream_t s, bool *used) {
     *used = false;
-    static const char *dir = std::getenv("SH_HSACO_DIR");
+#ifdef SH_MEASUREMENT_BUILD
+    static const char *dir = SH_MEASURE_ENV("SH_HSACO_DIR");
     if (!dir) return hipSuccess;
     static std::mutex mu;
     static std::map<std::string, hipFunction_t> fns;
@@ -53,6 +56,10 @@ hipError_t module_launch(const char *tag, const FixedArgs &a, unsigned blocks, u
     size_t sz = sizeof(arg);
     void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &arg, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
     return hipModuleLaunchKernel(f, blocks, 1, 1, threads, 1, 1, static_cast<unsigned>(lds), s, nullptr, cfg);
+#else
+    (void)tag, (void)a, (void)blocks, (void)threads, (void)lds, (void)s;
+    return hipSuccess;
+#endif
 }
 }  // namespace fixed
 

@@ -11,6 +11,7 @@
 // outputs are unframed on the host threads. So host framing, PCIe and kernels overlap, and the
 // only host work per byte is the framing copy the reference also does (its memset/memcpy).
 #include <hip/hip_runtime.h>
+#include <sched.h>
 #include <emmintrin.h>
 
 #include <algorithm>
@@ -26,6 +27,7 @@
 #include <vector>
 
 #include "../../include/cauchy_256_batch.h"
+#include "measure.hpp"
 #include "../../include/shorthair_groups.h"
 
 namespace {
@@ -33,7 +35,7 @@ namespace {
 // device bytes per chunk (inputs + outputs); SH_PKT_CHUNK_MB: measurement switch
 size_t chunk_bytes() {
     static const size_t b = [] {
-        const char *e = std::getenv("SH_PKT_CHUNK_MB");
+        const char *e = SH_MEASURE_ENV("SH_PKT_CHUNK_MB");
         const int mb = e ? std::atoi(e) : 48;
         return static_cast<size_t>(std::max(1, mb)) << 20;
     }();
@@ -81,8 +83,13 @@ inline void framing_fence() { _mm_sfence(); }
 
 int host_threads() {
     static const int n = [] {
-        const char *e = std::getenv("SH_HOST_THREADS");
-        int v = e ? std::atoi(e) : static_cast<int>(std::thread::hardware_concurrency());
+        // the cores this process may run on (its affinity mask: a job's share of a large host),
+        // at most 16; SH_HOST_THREADS overrides it in measurement builds only
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        int v = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set)
+                                                            : static_cast<int>(std::thread::hardware_concurrency());
+        if (const char *e = SH_MEASURE_ENV("SH_HOST_THREADS")) v = std::atoi(e);
         return std::max(1, std::min(v > 0 ? v : 1, 16));
     }();
     return n;
@@ -99,9 +106,16 @@ class Workers {
         for (auto &t : th_) t.detach();
     }
     int size() const { return nthreads_; }
-    // fn(i) for i in [0, n) split into t <= size() contiguous ranges; the caller runs range 0
+    // fn(i) for i in [0, n) split into t <= size() contiguous ranges; the caller runs range 0.
+    // One pass owns the pool at a time; a pass from another thread that finds it busy runs its
+    // whole range on its own thread instead of queueing behind the owner, so
+    // concurrent shorthair_*_groups calls still overlap.
     void run(int n, int t, const std::function<void(int)> &fn) {
-        std::lock_guard<std::mutex> one(run_mu_);  // one pass at a time
+        std::unique_lock<std::mutex> one(run_mu_, std::try_to_lock);
+        if (!one.owns_lock() || t <= 1) {
+            for (int i = 0; i < n; ++i) fn(i);
+            return;
+        }
         {
             std::lock_guard<std::mutex> g(mu_);
             fn_ = &fn;

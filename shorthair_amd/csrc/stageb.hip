@@ -20,6 +20,7 @@
 
 #include "kernels.hpp"
 #include "snippets.h"
+#include "measure.hpp"
 
 #include <algorithm>
 #include <cstdlib>
@@ -681,7 +682,7 @@ hipError_t launch_stageb_v2(const StageBV2Args &a, hipStream_t stream) {
     // (200,56,1352) stage B 0.478 vs 0.532 ms (7 waves), (190,66,1336) 0.763 vs 0.838 ms
     // (stageb_fixed), (120,136,1400) 1.772 vs 2.070 ms (4096 groups).
     // One or two output octets (emax <= 16): one workgroup of as many waves, no idle waves.
-    static const int force = std::getenv("SH_V2_NW") ? std::atoi(std::getenv("SH_V2_NW")) : 0;  // measurement
+    static const int force = sh::measure_int(SH_MEASURE_ENV("SH_V2_NW"), 0);  // measurement
     const int c4 = (octets + 3) / 4, c8 = (octets + 7) / 8;
     const int nw = (force == 1 || force == 2) && octets <= 2 ? force                       // 1-2 waves hold <= 16 rows
                    : (force == 4 || force == 8) ? force
@@ -689,7 +690,7 @@ hipError_t launch_stageb_v2(const StageBV2Args &a, hipStream_t stream) {
     // A last chunk with fewer octets than waves (e = 66: 3 x 4 waves, the third with one active
     // wave) runs as its own launch of 1- or 2-wave workgroups instead: no idle waves holding
     // registers and barrier slots (SH_V2_NO_TAIL: measurement switch).
-    static const bool no_tail = std::getenv("SH_V2_NO_TAIL") != nullptr;
+    static const bool no_tail = SH_MEASURE_ENV("SH_V2_NO_TAIL") != nullptr;
     // One 8-wave chunk with 5 or 6 octets (e = 33..48): a 4-wave chunk plus a 1-2-wave tail.
     const int nw1 = (!no_tail && force == 0 && nw == 8 && (octets == 5 || octets == 6)) ? 4 : nw;
     int chunks = (octets + nw1 - 1) / nw1;
@@ -851,7 +852,7 @@ hipError_t launch_stageb_small(const StageBSmallArgs &a, hipStream_t stream) {
     if (!stageb_small_ok(a.geo, a.emax)) return hipErrorNotSupported;
     const int gpw = 64 / a.geo.nq;
     const int ngb = (a.groups + gpw - 1) / gpw, nch = (a.emax + 7) / 8;
-    static const bool xcd = !std::getenv("SH_SMALL_XCD") || std::atoi(std::getenv("SH_SMALL_XCD")) != 0;  // measurement
+    static const bool xcd = sh::measure_int(SH_MEASURE_ENV("SH_SMALL_XCD"), 1) != 0;  // measurement
     StageBSmallArgs m = a;
     m.xcd_map = xcd && nch > 1 ? 1 : 0;
     const dim3 grid = m.xcd_map ? dim3(static_cast<unsigned>(8 * nch * ((ngb + 7) / 8)), 1, 1)

@@ -40,7 +40,7 @@ typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 
 template <int P_, int CW_>
 struct TShape {
-    static constexpr int P = P_, CW = CW_, W = 16;
+    static constexpr int P = P_, CW = CW_, W = 16, PW = P_;  // all parts in one workgroup
     static constexpr int NW = CW * P, NT = 64 * NW, COLS = CW * 64;
     static constexpr int ROWB = COLS * 4, SLOT = 8 * ROWB, IMG = SLOT;
     static constexpr int NDMA = SLOT / (64 * W);

@@ -66,6 +66,43 @@ def test_field_table_pointers_exported():
     assert ctypes.c_void_p.in_dll(shorthair_amd.lib, "GFC256_MUL_TABLE").value is None
 
 
+# Environment switches that select other kernels or launch splits for same-box A/B runs. They
+# exist only in measurement builds (tools/build_variant.sh, csrc/measure.hpp); the shipped drop-in
+# library must not change its code path because of its caller's environment.
+MEASUREMENT_SWITCHES = ("SH_HSACO_DIR", "SH_DEC_CHUNKS", "SH_STAGEB_OLD", "SH_FORCE_TILE", "SH_NO_TILE",
+                        "SH_NO_COL", "SH_COL_ENC", "SH_SB_SLICE", "SH_SLICE_MAX", "SH_SLICE_STEPS",
+                        "SH_SMALL_XCD", "SH_V2_NW", "SH_V2_NO_TAIL", "SH_V2_MIN", "SH_V2_MAX",
+                        "SH_PKT_CHUNK_MB", "SH_HOST_THREADS")
+
+
+def test_product_library_has_no_measurement_hooks():
+    """The default libcauchy256.so names none of the A/B switches, imports no module loader and
+    reads no environment variable at all."""
+    import shorthair_amd
+    blob = open(shorthair_amd.LIB_PATH, "rb").read()
+    for name in MEASUREMENT_SWITCHES:
+        assert name.encode() not in blob, name
+    out = subprocess.run(["nm", "-D", "--undefined-only", shorthair_amd.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    undefined = {line.split()[-1].split("@")[0] for line in out.splitlines() if line.strip()}
+    assert not any(u.startswith("hipModule") for u in undefined), sorted(u for u in undefined if "Module" in u)
+    assert "getenv" not in undefined and "secure_getenv" not in undefined
+
+
+def test_measurement_switches_only_behind_the_build_flag():
+    """Every getenv in the library sources goes through csrc/measure.hpp's SH_MEASURE_ENV (a null
+    pointer unless -DSH_MEASUREMENT_BUILD), and only variant builds set that flag."""
+    csrc = os.path.join(ROOT, "shorthair_amd", "csrc")
+    for f in os.listdir(csrc):
+        if f.endswith((".cpp", ".hip", ".hpp", ".h")) and f != "measure.hpp":
+            text = open(os.path.join(csrc, f)).read()
+            assert "getenv" not in text, f
+            assert "hipModuleLoad" not in text or "#ifdef SH_MEASUREMENT_BUILD" in text, f
+    build = open(os.path.join(ROOT, "shorthair_amd", "build.py")).read()
+    assert 'os.environ.get("SH_MEASUREMENT") == "1"' in build
+    assert "SH_MEASUREMENT=1" in open(os.path.join(ROOT, "tools", "build_variant.sh")).read()
+
+
 def test_headers_have_no_torch_or_cpp_types():
     for h in os.listdir(INCLUDE):
         text = re.sub(r"/\*.*?\*/", " ", open(os.path.join(INCLUDE, h)).read(), flags=re.S)

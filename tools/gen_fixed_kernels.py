@@ -535,6 +535,14 @@ def shape(k, m):
     return P, CW, R, minw, sync
 
 
+def parts_per_wg(P):
+    """Parts per workgroup (fixed_common.hpp Shape::PW). A/B switch SH_PW: the P parts of a tile
+    run in P / SH_PW workgroups, each with its own ring over the whole tile (one or two code
+    streams per workgroup for P / PW times the input reads through L2). Default: all P."""
+    pw = int(os.environ.get("SH_PW", "0")) or P
+    return pw if P % pw == 0 else P
+
+
 PERSIST = os.environ.get("SH_PERSIST", "0") == "1"
 # Decode stage A, SH_RINIT=1 (measured, not the default): residual rows start as the recovery
 # blocks R_y, loaded into the accumulators in the prologue (Src::rrow) instead of m extra ring
@@ -651,7 +659,8 @@ def gen_config(k, m):
                     f'#include "fixed_{name}.inc"\n'
                     + (f"FIXED_KERNEL_PERSISTENT({name}, {k}, {m}, {P}, {CW}, {R}, {minw}, {mode}, {dec})\n" if pers[mode] else
                        f"FIXED_KERNEL({name}, {k}, {m}, {P}, {CW}, {R}, {minw}, {mode}, {dec}, "
-                       f"{'false' if 'nodma' in ABLATE else 'true'}, {'true' if stream_mode(P) else 'false'})\n"))
+                       f"{'false' if 'nodma' in ABLATE else 'true'}, {'true' if stream_mode(P) else 'false'}, "
+                       f"{parts_per_wg(P)})\n"))
         paths.append(path)
     return paths
 
