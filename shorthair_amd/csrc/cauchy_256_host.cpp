@@ -90,6 +90,10 @@ struct StreamState {
     std::mutex mu;
     DevBuf ws;
     int *d_errors = nullptr;
+    // split-tile scratch of the compile-time kernels (lease_split), its own lock: a decode holds
+    // `mu` while it launches stage A, which takes this one too
+    std::mutex split_mu;
+    DevBuf split;
 };
 
 // One launch of the tile kernels: output rows [row0, row0 + nrows) with its snippet-address table.
@@ -252,6 +256,41 @@ int lease_workspace(Context &c, hipStream_t stream, size_t bytes, WsLease &out, 
     return 0;
 }
 
+// Split-tile scratch of a stream (fixed_common.hpp RowSink "Split tiles": the last tiles of a
+// compile-time launch run as two half-step workgroups whose partial rows meet here): 64 MB of
+// partials and one arrival counter per split tile, zeroed once when allocated (every launch
+// leaves them zero: the second arriver resets its tile's). Locked for one launch; launches on one
+// stream are ordered by the stream.
+constexpr size_t kSplitPartBytes = 64ull << 20;
+constexpr int kSplitMinGroups = 16;  // smaller batches: whole tiles (no scratch for the stream)
+// Only the A/B builds generate split-tile programs (tools/gen_fixed_kernels.py SH_SPLIT_GEN=1,
+// measured no faster: profiles/r06/ab_runs.txt block 2); the product never leases the scratch.
+#ifdef SH_MEASUREMENT_BUILD
+constexpr bool kSplitLaunch = true;
+#else
+constexpr bool kSplitLaunch = false;
+#endif
+constexpr int kSplitCounters = 4096;
+struct SplitLease {
+    std::unique_lock<std::mutex> lk;
+    uint8_t *part = nullptr;
+    uint32_t *cnt = nullptr;
+};
+int lease_split(Context &c, hipStream_t stream, SplitLease &out) {
+    StreamState *st = stream_state(c, stream);
+    if (!st) return -2;
+    out.lk = std::unique_lock<std::mutex>(st->split_mu);
+    if (!st->split.p) {
+        if (st->split.ensure(kSplitPartBytes + kSplitCounters * sizeof(uint32_t), stream)) return -2;
+        if (hipMemsetAsync(static_cast<uint8_t *>(st->split.p) + kSplitPartBytes, 0,
+                           kSplitCounters * sizeof(uint32_t), stream) != hipSuccess)
+            return -2;
+    }
+    out.part = static_cast<uint8_t *>(st->split.p);
+    out.cnt = reinterpret_cast<uint32_t *>(out.part + kSplitPartBytes);
+    return 0;
+}
+
 // Device generator for (k, m), m >= 2, k + m <= 256. Cached; created once per shape.
 uint8_t *generator(Context &c, int k, int m) {
     std::lock_guard<std::mutex> g(c.mu);
@@ -380,10 +419,17 @@ hipStream_t pick(void *stream) { return static_cast<hipStream_t>(stream); }
 
 // One launch of a compile-time-scheduled kernel over the whole batch (the kernels build their
 // buffer descriptors per workgroup, so 32-bit offsets never limit the batch size).
+// split: the stream's split-tile scratch (nullptr: whole tiles only).
 hipError_t launch_fixed_batch(int k, int m, int B, int groups, const uint8_t *in, long long in_gs,
                               uint8_t *out, long long out_gs, const uint8_t *pos,
-                              const uint8_t *rpos, bool dec, hipStream_t s) {
+                              const uint8_t *rpos, bool dec, hipStream_t s, const SplitLease *split = nullptr) {
     sh::FixedArgs a{};
+    if (split) {
+        a.split_part = split->part;
+        a.split_cnt = split->cnt;
+        a.split_cap = static_cast<long long>(kSplitPartBytes);
+        a.split_max = kSplitCounters;
+    }
     a.in = in;
     a.in_gstride = in_gs;
     a.in_bytes = static_cast<long long>(groups) * in_gs;
@@ -485,8 +531,12 @@ int encode_batch(int k, int m, int B, int groups, const uint8_t *d_in, uint8_t *
     }
     const bool sliced = slice_scratch && groups == 1 && tile_usable(c, k, m, B) && latency_slices(k) > 1;
     if (sh::has_fixed(k, m, B) && !force_tile() && !sliced) {
+        SplitLease sp;
+        const bool split = kSplitLaunch && groups >= kSplitMinGroups;
+        if (split)
+            if (int rc = lease_split(c, s, sp)) return rc;
         SH_CHECK(launch_fixed_batch(k, m, B, groups, d_in, in_gs, d_out, out_gs, nullptr, nullptr,
-                                    false, s));
+                                    false, s, split ? &sp : nullptr));
         return 0;
     }
     if (tile_usable(c, k, m, B))
@@ -720,8 +770,13 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
         //   residual_y = R_y + sum_{received x} M(C[y][x]) d_x
         const bool sliced = slice_scratch && groups == 1 && tile_usable(c, k, m, B) && latency_slices(k + m) > 1;
         if (sh::has_fixed(k, m, B) && !force_tile() && !sliced) {
+            SplitLease sp;
+            const bool split = kSplitLaunch && groups >= kSplitMinGroups;
+            if (split)
+                if (int rc = lease_split(c, s, sp)) return rc;
             SH_CHECK(launch_fixed_batch(k, m, B, groups, d_blocks, static_cast<long long>(k) * B,
-                                        w.residual, static_cast<long long>(m) * B, w.pos, w.rpos, true, s));
+                                        w.residual, static_cast<long long>(m) * B, w.pos, w.rpos, true, s,
+                                        split ? &sp : nullptr));
         } else if (int rc = launch_tile_batch(c, k, m, B, groups, d_blocks, static_cast<long long>(k) * B,
                                               w.residual, static_cast<long long>(m) * B, w.pos, w.rpos, true, s,
                                               sliced ? slice_scratch : nullptr)) {

@@ -45,6 +45,7 @@
 #include <stdint.h>
 
 #include "geometry.hpp"
+#include "measure.hpp"
 
 #include <algorithm>
 #include <type_traits>
@@ -100,7 +101,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wg_rsrc(const uint8_t *base, l
 // PW_ = parts per workgroup (default all P): with PW < P the P parts of a tile run in H = P / PW
 // workgroups, each reading the whole tile through its own ring (generator switch SH_PW, A/B
 // builds: fewer code streams per workgroup for H times the input reads).
-template <int K_, int M_, int P_, int CW_, int R_, bool DMA_ = true, int PW_ = P_>
+// SLOTB_ > 0: ring slots of that many bytes instead of one row image (BlkSrc's whole-block slots).
+template <int K_, int M_, int P_, int CW_, int R_, bool DMA_ = true, int PW_ = P_, int SLOTB_ = 0>
 struct Shape {
     static constexpr int K = K_, M = M_, P = P_, CW = CW_, R = R_, W = 16;
     static constexpr int PW = PW_, H = P_ / PW_;
@@ -109,7 +111,7 @@ struct Shape {
     static constexpr int NW = CW * PW, NT = 64 * NW, COLS = CW * 64;
     static constexpr int ROWB = COLS * 4;               // bytes of one sub-block row of a slot
     static constexpr int IMG = 8 * ROWB;                // bytes of one epilogue row image
-    static constexpr int SLOT = IMG;                    // bytes per ring slot (one input block)
+    static constexpr int SLOT = SLOTB_ > 0 ? SLOTB_ : IMG;  // bytes per ring slot (one input block)
     static constexpr int NDMA = SLOT / (64 * W);        // DMA wave-instructions per step
     static constexpr int DPW = (NDMA + NW - 1) / NW;    // ... issued by each wave (at most)
     static constexpr int KP = (K + 3) & ~3, MP = (M + 3) & ~3;
@@ -158,7 +160,7 @@ __device__ __forceinline__ WGInfo tile_info(int nq, long long col0, long long lo
 
 template <class S, bool DEC>
 struct Src {
-    static constexpr bool kStream = false;
+    static constexpr bool kStream = false, kBlk = false;
     __amdgpu_buffer_rsrc_t rsrc;
     uint32_t dbase[S::DPW];   // chunk source offset, block 0 / array slot 0 (OOR past the batch)
     int dgl[S::DPW];          // decode: the chunk's group (position-table index)
@@ -182,6 +184,9 @@ struct Src {
                                     // staged into the LDS copy at this tile's end)
     uint32_t lbase;           // decode: this lane's column in its group (OOR: past the batch)
     int lgl;                  // ... and its group (position-table index)
+    // encode: byte offset of step 0's block (the second half of a split tile starts at block x0)
+    mutable uint32_t boff = 0;
+    __device__ __forceinline__ void set_step0(int x0) const { boff = static_cast<uint32_t>(x0) * B; }
 
     __device__ __forceinline__ static void chunk_src(const Geometry &geo, long long in_gstride_, const WGInfo &w,
                                                      uint32_t (&db)[S::DPW], int (&gl)[S::DPW]) {
@@ -380,7 +385,7 @@ struct Src {
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, S::W, o, 0, 0, SH_LOAD_AUX);
             } else {
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, S::W, dbase[j],
-                                                         static_cast<uint32_t>(x) * B, 0, SH_LOAD_AUX);
+                                                         static_cast<uint32_t>(x) * B + boff, 0, SH_LOAD_AUX);
             }
         }
     }
@@ -401,6 +406,181 @@ struct Src {
 
 };
 
+// Whole-block input (generator switch SH_BLK=<sub>, a kernel for one block size B = 8 * SUB;
+// VERDICT r5 #2). The DMA reads each group the tile touches as ONE run of consecutive 16-byte
+// chunks -- the group's whole block, 16-byte aligned in LDS at a stride GS -- instead of 175-byte
+// sub-block rows realigned per lane (Src): the DMA's cost follows its runs of strictly
+// consecutive chunks (reads alone 0.37 vs 0.42 ms, profiles/r05/ab_runs.txt block 2). A slot is
+// then the raw image of up to NG blocks, and a lane's word of sub-block a sits at byte
+// gl * GS + a * SUB + 4q: for a * SUB % 4 != 0 it is read as the two covering dwords and
+// realigned with one v_alignbyte_b32 whose shift (a * SUB % 4) is a compile-time constant --
+// round 5's version read it with byte-unaligned ds_read_b32 (~48 LDS cycles each, 5.3x slower).
+// Column q = nq - 1 is read unshifted (bytes 4q..4q+3 of the sub-block, the last of them the
+// next sub-block's first byte): the garbage byte lands in output byte SUB of each sub-block,
+// which RowSink never stores (its last piece is realigned instead, RowSink::kBlk).
+// GS: 16-byte multiple with GS/4 = nq (mod 32), so 32 consecutive tile columns hit 32 banks.
+template <int SUB>
+struct BlkGeo {
+    static constexpr int NQ = ((SUB + 3) / 4 + 3) & ~3;
+    static constexpr int B = 8 * SUB;
+    static constexpr int CH = (B + 15) / 16;  // DMA chunks per block
+    static constexpr int gs_of(int g) { return ((g / 4) % 32 == NQ % 32) ? g : gs_of(g + 16); }
+    static constexpr int GS = gs_of((B + 15) & ~15);
+    static constexpr int CPG = GS / 16;       // chunk slots per group image
+    static constexpr int NG = (127 + NQ - 1) / NQ + 1;  // groups a 128-column tile can touch
+    static constexpr int SLOT = ((NG * GS + 1023) / 1024) * 1024;
+    static_assert(SUB >= 16 && NQ >= 8, "block size");
+    // Tile starts. RowSink's last piece of a sub-block needs the byte before it from column
+    // nq - 5 (BlkSrc reads the last chunk unshifted), so no tile may start at column nq - 4 of a
+    // group: such a tile starts 4 columns earlier instead (those 4 columns are computed and
+    // stored by both neighbours, with equal values). With 128 = -4 (mod 44) that happens once
+    // per 10 tiles at B = 1400. The starts repeat with a period of PT tiles spanning D columns.
+    static constexpr int next_start(int c) { return (c + 128) % NQ == NQ - 4 ? c + 124 : c + 128; }
+    static constexpr int period() {
+        int c = next_start(0), t = 1;
+        while (c % NQ != 0) c = next_start(c), ++t;
+        return t;
+    }
+    static constexpr int PT = period();
+    struct Starts {
+        int off[PT];
+        int span;
+    };
+    static constexpr Starts starts() {
+        Starts r{};
+        int c = 0;
+        for (int t = 0; t < PT; ++t) r.off[t] = c, c = next_start(c);
+        r.span = c;
+        return r;
+    }
+    __host__ __device__ static long long tile_start(int t) {
+        constexpr Starts st = starts();
+        return static_cast<long long>(st.span) * (t / PT) + st.off[t % PT];
+    }
+    __host__ __device__ static int tiles(long long cols) {
+        constexpr Starts st = starts();
+        const long long full = cols / st.span, rem = cols - full * st.span;
+        int n = static_cast<int>(full) * PT;
+        for (int t = 0; t < PT; ++t) n += st.off[t] < rem;
+        return n;
+    }
+};
+
+template <class S, bool DEC, int SUB>
+struct BlkSrc {
+    using G = BlkGeo<SUB>;
+    static constexpr bool kStream = false, kBlk = true;
+    static_assert(S::SLOT == G::SLOT && S::COLS == 128, "whole-block slots (generator SH_BLK)");
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t dbase[S::DPW];   // chunk source offset, block 0 / array slot 0 (OOR: none)
+    int dgl[S::DPW];          // decode: the chunk's group (position-table index)
+    int wave;
+    uint32_t rd;              // this lane's word of sub-block 0 in a slot: gl * GS + 4q
+    const uint8_t *lds;
+    const uint8_t *pos;
+    mutable uint32_t boff = 0;  // as Src::boff
+    __device__ __forceinline__ void set_step0(int x0) const { boff = static_cast<uint32_t>(x0) * G::B; }
+
+    __device__ __forceinline__ void init(const FixedArgs &a, const WGInfo &w, const uint8_t *lds_ring,
+                                         const uint8_t *lds_pos) {
+        rsrc = wg_rsrc(a.in, a.in_bytes, a.in_gstride, w.g_first);
+        lds = lds_ring;
+        pos = lds_pos;
+        wave = w.wave;
+        rd = w.valid ? static_cast<uint32_t>(w.gl * G::GS + 4 * w.q) : 0u;
+        const long long tlo = w.col0 > w.lo ? w.col0 : w.lo;
+        const long long thi = w.col0 + S::COLS < w.hi ? w.col0 + S::COLS : w.hi;
+        const int ng = thi > tlo ? static_cast<int>((thi - 1) / G::NQ) - w.g_first + 1 : 0;
+        const uint32_t gstride = static_cast<uint32_t>(a.in_gstride);
+#pragma unroll
+        for (int j = 0; j < S::DPW; ++j) {
+            const int ci = (w.wave * S::DPW + j) * 64 + w.lane;  // chunk slot in the image
+            const int gl = ci / G::CPG, ch = ci - gl * G::CPG;
+            dgl[j] = gl < ng ? gl : 0;
+            dbase[j] = (gl < ng && ch < G::CH) ? static_cast<uint32_t>(gl) * gstride + 16u * ch : OOR;
+        }
+    }
+    template <int T, int I, int EX = 0>
+    __device__ __forceinline__ void wait() const {
+        constexpr int N = (I - T - 1) * S::DPW;
+        static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+        if (S::NDMA % S::NW != 0 && wave * S::DPW >= S::NDMA)
+            asm volatile("s_barrier" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+    }
+    __device__ __forceinline__ static void release() {
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    struct Pre {
+        int p[S::DPW];
+    };
+    __device__ __forceinline__ Pre pre(int t) const {
+        Pre r;
+#pragma unroll
+        for (int j = 0; j < S::DPW; ++j) r.p[j] = DEC ? pos[dgl[j] * (S::KP + S::MP) + t] : 0;
+        return r;
+    }
+    struct Pre4 {
+        uint32_t w[S::DPW];
+    };
+    __device__ __forceinline__ Pre4 pre4(int t) const {
+        Pre4 r;
+#pragma unroll
+        for (int j = 0; j < S::DPW; ++j) {
+            r.w[j] = 0;
+            if (DEC) r.w[j] = *reinterpret_cast<const u32_ua *>(pos + dgl[j] * (S::KP + S::MP) + t);
+        }
+        return r;
+    }
+    __device__ __forceinline__ void issue4(int x, const Pre4 &p4, int i) const {
+        Pre r;
+#pragma unroll
+        for (int j = 0; j < S::DPW; ++j) r.p[j] = static_cast<int>((p4.w[j] >> (8 * i)) & 0xFFu);
+        issue(x, r);
+    }
+    __device__ __forceinline__ void issue(int x, const Pre &pr) const {
+        uint8_t *slot = const_cast<uint8_t *>(lds) + (x % S::R) * S::SLOT;
+#pragma unroll
+        for (int j = 0; j < S::DPW; ++j) {
+            if (S::NDMA % S::NW != 0 && wave * S::DPW + j >= S::NDMA) break;  // uniform
+            lds_void *dst = (lds_void *)(slot + (wave * S::DPW + j) * 64 * S::W);
+            if (DEC) {
+                const int p = pr.p[j];
+                const uint32_t o = (p == 0xFF || dbase[j] == OOR) ? OOR : dbase[j] + static_cast<uint32_t>(p) * G::B;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, S::W, o, 0, 0, SH_LOAD_AUX);
+            } else {
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, S::W, dbase[j],
+                                                         static_cast<uint32_t>(x) * G::B + boff, 0, SH_LOAD_AUX);
+            }
+        }
+    }
+    template <int A>
+    __device__ __forceinline__ static uint32_t word(const uint8_t *p) {
+        constexpr int off = A * SUB, al = off & ~3, sh = off & 3;
+        const uint32_t lo = *reinterpret_cast<const uint32_t *>(p + al);
+        if constexpr (sh == 0) {
+            return lo;
+        } else {
+            const uint32_t hi = *reinterpret_cast<const uint32_t *>(p + al + 4);
+            return __builtin_amdgcn_alignbyte(hi, lo, sh);
+        }
+    }
+    __device__ __forceinline__ void read(int slot, uint32_t &d0, uint32_t &d1, uint32_t &d2,
+                                         uint32_t &d3, uint32_t &d4, uint32_t &d5, uint32_t &d6,
+                                         uint32_t &d7) const {
+        const uint8_t *p = lds + slot * S::SLOT + rd;
+        d0 = word<0>(p);
+        d1 = word<1>(p);
+        d2 = word<2>(p);
+        d3 = word<3>(p);
+        d4 = word<4>(p);
+        d5 = word<5>(p);
+        d6 = word<6>(p);
+        d7 = word<7>(p);
+    }
+};
+
 // One-part shapes (P = 1): nothing is shared between the waves of a workgroup -- each column-wave
 // alone consumes its columns -- so the LDS ring is pure overhead there: its DMA, the round trip
 // through LDS and a workgroup barrier every step (the (28,4) ring holds only 4 slots of 16 KB).
@@ -410,13 +590,15 @@ struct Src {
 // and no wave waits for another until the epilogue's row images.
 template <class S, bool DEC>
 struct StreamSrc {
-    static constexpr bool kStream = true;
+    static constexpr bool kStream = true, kBlk = false;
     __amdgpu_buffer_rsrc_t rsrc;
     uint32_t lane_base;       // this lane's column in its group (OOR: past the batch)
     int gl;                   // decode: the lane's group (position-table index)
     uint32_t B, sub;
     const uint8_t *pos;
     mutable uint32_t buf[S::R][8];  // step x in buf[x % R] (compile-time indices after inlining)
+    mutable uint32_t boff = 0;      // as Src::boff
+    __device__ __forceinline__ void set_step0(int x0) const { boff = static_cast<uint32_t>(x0) * B; }
 
     __device__ __forceinline__ void init(const FixedArgs &a, const WGInfo &w, const uint8_t *, const uint8_t *lds_pos) {
         const Geometry &geo = a.geo;
@@ -464,7 +646,7 @@ struct StreamSrc {
         if (DEC)
             o = (pr.p == 0xFF || lane_base == OOR) ? OOR : lane_base + static_cast<uint32_t>(pr.p) * B;
         else
-            so = static_cast<uint32_t>(x) * B;
+            so = static_cast<uint32_t>(x) * B + boff;
 #pragma unroll
         for (int s = 0; s < 8; ++s)
             buf[x % S::R][s] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, o == OOR ? OOR : o + s * sub, so, SH_LOAD_AUX);
@@ -494,11 +676,25 @@ struct StreamSrc {
 // reads row y's image before it joins row y+1's barrier, so row y+2 may overwrite it.
 // Every wave of the workgroup joins one barrier per row of the largest part (pad() for the
 // shorter parts). The images ([2][PW][SLOT] bytes) alias the ring (after Src::release()).
-template <class S>
+// BLK (BlkSrc inputs): the words of a sub-block's last chunk were computed unshifted (bytes
+// 4q..4q+3), so that piece (stored at sub - 16, as always) is taken from the image one byte
+// earlier: five aligned dwords from lsrc - 4, realigned by v_alignbyte_b32 with shift 3 (shift 0,
+// read from lsrc, for every other piece: one code path for all lanes).
+template <class S, bool BLK = false>
 struct RowSink {
     __amdgpu_buffer_rsrc_t rsrc;
     mutable uint32_t gdst[2];  // per piece: destination offset without the row term (OOR: none)
     mutable uint32_t lsrc[2];  // per piece: byte offset inside a row image
+    mutable uint32_t lsh[2];   // BLK: per piece byte shift (3: last chunk of its sub-block)
+    mutable uint32_t poff[2];  // split tiles: per piece offset in a partial row (piece index * 16)
+    // Split tiles (see "Split tiles" below): this workgroup computes half `half` of the steps of
+    // split tile `sidx`; its rows go to the partial scratch, the second arriver combines.
+    __amdgpu_buffer_rsrc_t prsrc;
+    uint32_t pbase;            // this split tile's partials: [half][M rows][2 * COLS pieces][16 B]
+    uint32_t *cnt;             // its arrival counter (zero between launches)
+    int half;
+    uint8_t *lds0;             // workgroup LDS base (the combine's "last arriver" word)
+    static constexpr uint32_t PR = 32u * S::COLS;  // bytes of one partial row (2 * COLS pieces)
     mutable uint32_t wofs;     // this lane's word in a row image (tile column * 4)
     uint32_t B;
     uint8_t *img;              // this part's row image, even rows (odd rows: + P * SLOT)
@@ -545,8 +741,10 @@ struct RowSink {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             int rem = (cw * 2 + h) * 64 + lane;  // piece index in memory order
+            poff[h] = static_cast<uint32_t>(rem) * 16u;
             gdst[h] = OOR;
             lsrc[h] = 0;
+            lsh[h] = 0;
             long long g;
             int b, q;
             bool ok;
@@ -570,20 +768,86 @@ struct RowSink {
                 gdst[h] = static_cast<uint32_t>(g - g_first) * out_gstride +
                           col_off(q, geo) + static_cast<uint32_t>(b * geo.sub);
                 lsrc[h] = static_cast<uint32_t>(b * S::ROWB) + static_cast<uint32_t>(g * nq + q - col0) * 4u;
+                if (BLK && q == nq - 4 && 4 * nq != sub) {
+                    lsh[h] = 3;
+                    lsrc[h] -= 4;  // column nq - 5 is in the tile (BlkGeo::tile_start)
+                }
             }
         }
     }
+    // Row y's words into the row image (parity YI), barrier; then piece h of the image.
     template <int YI>
-    __device__ __forceinline__ void row(int y, const uint32_t (&w)[8]) const {
+    __device__ __forceinline__ uint8_t *image(const uint32_t (&w)[8]) const {
         uint8_t *im = img + (YI & 1) * S::PW * S::IMG;
 #pragma unroll
         for (int b = 0; b < 8; ++b) *reinterpret_cast<uint32_t *>(im + b * S::ROWB + wofs) = w[b];
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const u32x4 v = *reinterpret_cast<const u32x4 *>(im + lsrc[h]);
-            __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, gdst[h], static_cast<uint32_t>(y) * B, SH_STORE_AUX);
+        return im;
+    }
+    __device__ __forceinline__ u32x4 piece(const uint8_t *im, int h) const {
+        u32x4 v;
+        if constexpr (BLK) {
+            const uint32_t *p = reinterpret_cast<const uint32_t *>(im + lsrc[h]);
+            const uint32_t u0 = p[0], u1 = p[1], u2 = p[2], u3 = p[3], u4 = p[4];
+            v.x = __builtin_amdgcn_alignbyte(u1, u0, lsh[h]);
+            v.y = __builtin_amdgcn_alignbyte(u2, u1, lsh[h]);
+            v.z = __builtin_amdgcn_alignbyte(u3, u2, lsh[h]);
+            v.w = __builtin_amdgcn_alignbyte(u4, u3, lsh[h]);
+        } else {
+            v = *reinterpret_cast<const u32x4 *>(im + lsrc[h]);
         }
+        return v;
+    }
+    template <int YI>
+    __device__ __forceinline__ void row(int y, const uint32_t (&w)[8]) const {
+        const uint8_t *im = image<YI>(w);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            __builtin_amdgcn_raw_buffer_store_b128(piece(im, h), rsrc, gdst[h], static_cast<uint32_t>(y) * B, SH_STORE_AUX);
+    }
+
+    // ---- Split tiles. The launch's last tiles run as two workgroups each, one per half of the
+    // steps (blocks 0..n0-1 and n0..), so the grid's tail drains in half-tile tasks. Each half
+    // stores its rows' pieces as a partial (write-through sc1 stores, the whole tile's pieces in
+    // memory order, offset poff), drains them (every wave vmcnt(0)), meets the workgroup barrier,
+    // and one lane adds 1 to the tile's counter (relaxed, agent scope). The workgroup that draws 1
+    // is the second: it reads both partials with sc1 loads, XORs them (the bitmatrix product is
+    // linear in the steps) and stores the tile's rows; it then resets the counter. No workgroup
+    // waits for another, and the protocol holds for any placement of the two halves (the
+    // write-through hand-off of MI355X_MICROARCH.md "inter-workgroup visibility", first row);
+    // placing both on one XCD back to back (FIXED_KERNEL) only makes the second's reads cheaper.
+    __device__ __forceinline__ void split_init(const FixedArgs &a, int sidx, int h, uint8_t *lds) {
+        prsrc = make_rsrc(a.split_part, static_cast<uint32_t>(a.split_cap));
+        pbase = static_cast<uint32_t>(sidx) * 2u * S::M * PR;
+        cnt = a.split_cnt + sidx;
+        half = h;
+        lds0 = lds;
+    }
+    template <int YI>
+    __device__ __forceinline__ void part_row(int y, const uint32_t (&w)[8]) const {
+        const uint8_t *im = image<YI>(w);
+        const uint32_t so = pbase + static_cast<uint32_t>(half * S::M + y) * PR;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) __builtin_amdgcn_raw_buffer_store_b128(piece(im, h), prsrc, poff[h], so, 16 /* sc1 */);
+    }
+    // After every row of every part (part_row / pad): rows y0 .. y0 + nr - 1 are this wave's.
+    __device__ __forceinline__ void combine(int y0, int nr) const {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its partial
+        __syncthreads();
+        uint32_t *flag = reinterpret_cast<uint32_t *>(lds0);
+        if (threadIdx.x == 0) *flag = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if (*flag == 0) return;  // first arriver: the other half combines
+        for (int yi = 0; yi < nr; ++yi) {
+            const uint32_t y = static_cast<uint32_t>(y0 + yi);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const u32x4 p0 = __builtin_amdgcn_raw_buffer_load_b128(prsrc, poff[h], pbase + y * PR, 16);
+                const u32x4 p1 = __builtin_amdgcn_raw_buffer_load_b128(prsrc, poff[h], pbase + (S::M + y) * PR, 16);
+                __builtin_amdgcn_raw_buffer_store_b128(p0 ^ p1, rsrc, gdst[h], y * B, SH_STORE_AUX);
+            }
+        }
+        if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     template <int YI>
     __device__ __forceinline__ void pad() const {
@@ -681,9 +945,7 @@ __device__ __forceinline__ int xcd_tile(int b, int n) {
 // dispatch slots there, so the second to H-th reads of the tile's input hit that XCD's L2. The
 // grid is rounded up to a multiple of 8 * H; a block past the last tile returns -1.
 template <class S>
-__device__ __forceinline__ int tile_of(const FixedArgs &a, int &hgrp) {
-    const long long cols = static_cast<long long>(a.groups) * a.geo.nq;
-    const int ntiles = static_cast<int>((cols + S::COLS - 1) / S::COLS);
+__device__ __forceinline__ int tile_of(const FixedArgs &a, int &hgrp, int ntiles) {
     if (S::H == 1) {
         hgrp = 0;
         return xcd_tile(blockIdx.x, gridDim.x);
@@ -708,9 +970,35 @@ inline int persistent_slots() {
 // code object of that directory instead (tools/il_reorder.py layouts); *used = false: none.
 hipError_t module_launch(const char *tag, const FixedArgs &a, unsigned blocks, unsigned threads, size_t lds,
                          hipStream_t s, bool *used);
+// Whether a measurement build launches `tag` from an external code object (no split tiles then).
+bool tag_is_module(const char *tag);
 
-template <class S, bool DEC, bool STREAM = false, bool PERS = false>
-inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArgs), const char *tag = nullptr) {
+// Split tiles of a launch (RowSink "Split tiles"): about half a round of workgroup slots' worth
+// of the last tiles, so the grid drains in half-tile tasks; every tile when all halves fit one
+// round. A multiple of 8 (split_tile_of), at most what the caller's scratch holds, 0 below 8.
+// SH_SPLIT (measurement builds only) forces the count (0: no split).
+template <class S, bool DEC>
+inline int split_count(const FixedArgs &a, int ntiles, void (*kern)(FixedArgs), size_t lds) {
+    if (!a.split_part || !a.split_cnt || S::H != 1) return 0;
+    static const int slots = [&] {
+        int per_cu = 0, d = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, S::NT, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+        if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+            cus = 256;
+        return per_cu * (cus > 0 ? cus : 256);
+    }();
+    long long n = std::min<long long>(ntiles, slots / 2);
+    if (const char *e = SH_MEASURE_ENV("SH_SPLIT")) n = std::min<long long>(ntiles, std::atoi(e));
+    const long long per = 2ll * S::M * 32 * S::COLS;  // partial bytes per split tile
+    n = std::min<long long>(n, a.split_cap / per);
+    n = std::min<long long>(n, a.split_max);
+    n &= ~7ll;
+    return n >= 8 ? static_cast<int>(n) : 0;
+}
+
+template <class S, bool DEC, bool STREAM = false, bool PERS = false, bool SPLIT = false>
+inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArgs), const char *tag = nullptr,
+                               int ntiles = -1) {
     constexpr bool dec = DEC;
     a.groups_per_wg = (S::COLS - 1) / a.geo.nq + 2;
     // ring (the row images of the epilogue alias it); a streaming source needs only the images
@@ -719,8 +1007,10 @@ inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArg
     // (+4: Src::pre4 reads up to 3 bytes past the last group's table)
     const size_t lds = front + (dec ? static_cast<size_t>(a.groups_per_wg) * (S::KP + S::MP) + 4 : 0);
     const long long cols = static_cast<long long>(a.groups) * a.geo.nq;
-    unsigned blocks = static_cast<unsigned>((cols + S::COLS - 1) / S::COLS);  // one tile each
+    unsigned blocks = static_cast<unsigned>(ntiles >= 0 ? ntiles : (cols + S::COLS - 1) / S::COLS);  // one tile each
     if (S::H > 1) blocks = (blocks + 7) / 8 * 8 * S::H;  // tile_of(): H part-groups per tile
+    a.nsplit = (SPLIT && !PERS && !tag_is_module(tag)) ? split_count<S, DEC>(a, static_cast<int>(blocks), kern, lds) : 0;
+    blocks += static_cast<unsigned>(a.nsplit);  // split tiles: two workgroups each
     if (PERS) blocks = std::min<unsigned>(blocks, static_cast<unsigned>(persistent_slots()));
     if (tag) {
         bool used = false;
@@ -731,31 +1021,86 @@ inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArg
     return hipGetLastError();
 }
 
+// Tile of a workgroup when the launch's last `nsplit` tiles are split (a multiple of 8): blocks
+// [0, T - nsplit) are the whole tiles in xcd_tile order; block T - nsplit + j is half (j >> 3) & 1
+// of split tile xcd_tile(((j >> 4) << 3) | (j & 7), nsplit), so a tile's two halves get blocks 8
+// apart (one XCD, dispatched back to back) and run after every whole tile has been dispatched.
+__device__ __forceinline__ int split_tile_of(int ntiles, int nsplit, int &half, int &sidx) {
+    const int nfull = ntiles - nsplit;
+    if (static_cast<int>(blockIdx.x) < nfull) {
+        half = -1;
+        sidx = 0;
+        return xcd_tile(blockIdx.x, nfull);
+    }
+    const int j = static_cast<int>(blockIdx.x) - nfull, i = j >> 3;
+    half = i & 1;
+    sidx = xcd_tile(((i >> 1) << 3) | (j & 7), nsplit);
+    return nfull + sidx;
+}
+
+// Source of a kernel instance: StreamSrc (STREAM), BlkSrc (BLKSUB > 0: whole-block slots for
+// B = 8 * BLKSUB) or the sub-block-row gather Src.
+template <class S, bool DEC, bool STREAM, int BLKSUB>
+using SrcOf = typename std::conditional<
+    STREAM, StreamSrc<S, DEC>,
+    typename std::conditional<(BLKSUB > 0), BlkSrc<S, DEC, (BLKSUB > 0 ? BLKSUB : 64)>, Src<S, DEC>>::type>::type;
+
+// Tiles of a launch: COLS-column tiles, or BlkGeo's tile starts.
+template <class S, int BLKSUB>
+__host__ __device__ inline int tiles_of(long long cols) {
+    if constexpr (BLKSUB > 0)
+        return BlkGeo<BLKSUB>::tiles(cols);
+    else
+        return static_cast<int>((cols + S::COLS - 1) / S::COLS);
+}
+template <int BLKSUB>
+__device__ __forceinline__ long long tile_col0(int tile, int cols_per_tile) {
+    if constexpr (BLKSUB > 0)
+        return BlkGeo<BLKSUB>::tile_start(tile);
+    else
+        return static_cast<long long>(tile) * cols_per_tile;
+}
+
 }  // namespace fixed
 }  // namespace sh
 
 // One kernel + launcher of a generated (k, m): MODE enc (DEC = false) or dec (DEC = true);
 // MINW = waves per SIMD the registers are allocated for. The host routes shapes with
 // nq % 4 != 0 (a 16-byte chunk could straddle two groups) or sub < 16 to the generic kernel.
-#define FIXED_KERNEL(NAME, K, M, P, CW, R, MINW, MODE, DEC, DMA, STREAM, PW)                      \
+#define FIXED_KERNEL(NAME, K, M, P, CW, R, MINW, MODE, DEC, DMA, STREAM, PW, BLKSUB, SPLIT)       \
     namespace sh {                                                                                \
     namespace fixed {                                                                             \
+    using Shape_##NAME##_##MODE =                                                                 \
+        Shape<K, M, P, CW, R, DMA, PW, ((BLKSUB) > 0 ? BlkGeo<((BLKSUB) > 0 ? (BLKSUB) : 64)>::SLOT : 0)>; \
     __global__ __launch_bounds__(64 * CW * PW, MINW) void kern_##NAME##_##MODE(FixedArgs a) {     \
         extern __shared__ __attribute__((aligned(16))) uint8_t lds[];                             \
-        using S = Shape<K, M, P, CW, R, DMA, PW>;                                                 \
-        using SrcT = typename std::conditional<STREAM, StreamSrc<S, DEC>, Src<S, DEC>>::type;     \
+        using S = Shape_##NAME##_##MODE;                                                          \
+        using SrcT = SrcOf<S, DEC, STREAM, BLKSUB>;                                               \
         SrcT src;                                                                                 \
-        RowSink<S> sink;                                                                          \
-        int hgrp;                                                                                 \
-        const int tile = tile_of<S>(a, hgrp);                                                     \
-        if (tile < 0) return;                                                                     \
-        const long long c0 = static_cast<long long>(tile) * S::COLS;                              \
-        const int part = kernel_prologue<S, DEC>(a, lds, src, sink, c0, 0,                       \
-                                                 static_cast<long long>(a.groups) * a.geo.nq, 0, hgrp); \
-        run_##NAME##_##MODE(part, src, sink);                                                     \
+        RowSink<S, SrcT::kBlk> sink;                                                              \
+        const long long cols_ = static_cast<long long>(a.groups) * a.geo.nq;                      \
+        const int ntiles_ = tiles_of<S, BLKSUB>(cols_);                                           \
+        int hgrp = 0, half = -1, sidx = 0, tile;                                                  \
+        if ((SPLIT) && a.nsplit > 0) {                                                            \
+            tile = split_tile_of(ntiles_, a.nsplit, half, sidx);                                  \
+        } else {                                                                                  \
+            tile = tile_of<S>(a, hgrp, ntiles_);                                                  \
+            if (tile < 0) return;                                                                 \
+        }                                                                                         \
+        const long long c0 = tile_col0<BLKSUB>(tile, S::COLS);                                    \
+        const int part = kernel_prologue<S, DEC>(a, lds, src, sink, c0, 0, cols_, 0, hgrp);        \
+        if ((SPLIT) && half >= 0) {                                                               \
+            sink.split_init(a, sidx, half, lds);                                                  \
+            run_##NAME##_##MODE##_half(half, part, src, sink);                                    \
+        } else {                                                                                  \
+            run_##NAME##_##MODE(part, src, sink);                                                 \
+        }                                                                                         \
     }                                                                                             \
     hipError_t launch_##NAME##_##MODE(FixedArgs a, hipStream_t s) {                               \
-        return launch_shape<Shape<K, M, P, CW, R, DMA, PW>, DEC, STREAM>(a, s, kern_##NAME##_##MODE, #NAME "_" #MODE); \
+        if ((BLKSUB) > 0 && a.geo.B != 8 * (BLKSUB)) return hipErrorNotSupported;                 \
+        const long long cols_ = static_cast<long long>(a.groups) * a.geo.nq;                      \
+        return launch_shape<Shape_##NAME##_##MODE, DEC, STREAM, false, (SPLIT) != 0>(             \
+            a, s, kern_##NAME##_##MODE, #NAME "_" #MODE, tiles_of<Shape_##NAME##_##MODE, BLKSUB>(cols_)); \
     }                                                                                             \
     }                                                                                             \
     }

@@ -61,6 +61,16 @@ hipError_t module_launch(const char *tag, const FixedArgs &a, unsigned blocks, u
     return hipSuccess;
 #endif
 }
+
+bool tag_is_module(const char *tag) {
+#ifdef SH_MEASUREMENT_BUILD
+    static const char *dir = SH_MEASURE_ENV("SH_HSACO_DIR");
+    return dir && tag;
+#else
+    (void)tag;
+    return false;
+#endif
+}
 }  // namespace fixed
 
 bool has_fixed(int k, int m, int B) {

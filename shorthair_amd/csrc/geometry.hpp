@@ -50,6 +50,15 @@ struct FixedArgs {
     const uint8_t *pos;       // decode: [G][round4(k)] array index of original row x, 0xFF = erased
     const uint8_t *rpos;      // decode: [G][round4(m)] array index of recovery row y, 0xFF = absent
     int groups_per_wg;        // set by the launcher
+    // Tail split (fixed_common.hpp, "Split tiles"): the launch's last `nsplit` tiles run as two
+    // half-step workgroups each, combined in-launch. Host-provided scratch (per stream):
+    // split_part holds the halves' partial rows, split_cnt one arrival counter per split tile
+    // (zero between launches); split_cap = bytes of split_part. nsplit is set by the launcher.
+    uint8_t *split_part;
+    uint32_t *split_cnt;
+    long long split_cap;
+    int split_max;            // counters available (split tiles at most)
+    int nsplit;
 };
 
 }  // namespace sh

@@ -46,7 +46,7 @@ def test_part_layouts_fill_the_simds():
         assert (m + P - 1) // P <= 9
 
 
-def _symbolic_run(lines, k, nr):
+def _symbolic_run(lines, k, nr, x0=0):
     """Evaluate a generated part body symbolically: every 32-bit word is the XOR of a set of input
     sub-blocks, held as an int bitmask (bit 8x + a = sub-block a of input block x). Returns the
     accumulators [nr][8]. Reads follow the body's src.read(slot, ...) calls in order: the i-th read
@@ -64,7 +64,7 @@ def _symbolic_run(lines, k, nr):
         m = re.match(r"src\.read\((\d+), (.*)\);", ln)
         if m:
             for a, w in enumerate(m.group(2).split(",")):
-                env[w.strip()] = 1 << (8 * nread + a)
+                env[w.strip()] = 1 << (8 * (x0 + nread) + a)
             nread += 1
             continue
         m = re.match(r"const uint32_t (\w+) = X3\((\w+), (\w+), (\w+)\);", ln)
@@ -106,3 +106,25 @@ def test_scheduled_xor_programs_compute_the_bitmatrix(k, m, joint, monkeypatch):
             for b in range(8):
                 want = sum(g.row_bytes(rows[y0 + yi][x])[b] << (8 * x) for x in range(k))
                 assert acc[yi][b] == want, (y0 + yi, b)
+
+
+@pytest.mark.parametrize("k,m", [(20, 16), (28, 4), (200, 32)])
+def test_split_tile_halves_sum_to_the_product(k, m):
+    """Split tiles (fixed_common.hpp RowSink "Split tiles"): the two half-step programs the
+    generator emits (steps cut at an even index, as gen_config does) compute partial products that
+    XOR to the whole bitmatrix product -- what the second arriving workgroup stores."""
+    g = _gen()
+    rows = g.generator(k, m)
+    steps = [("c", x) for x in range(k)]
+    n0 = (len(steps) // 2) & ~1
+    y0, y1 = 0, min(m, 8)
+    parts = []
+    for sub, x0 in ((steps[:n0], 0), (steps[n0:], n0)):
+        body = g.Body(k, rows, y0, y1)
+        body.emit(16, 4, sub, (k + 3) & ~3)
+        parts.append(_symbolic_run(body.lines, len(sub), y1 - y0, x0))
+    for yi in range(y1 - y0):
+        for b in range(8):
+            want = sum(g.row_bytes(rows[y0 + yi][x])[b] << (8 * x) for x in range(k))
+            assert parts[0][yi][b] ^ parts[1][yi][b] == want, (yi, b)
+            assert parts[0][yi][b] >> (8 * n0) == 0  # half 0 touches blocks < n0 only

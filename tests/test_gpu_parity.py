@@ -107,8 +107,12 @@ def test_single_group_decode_abi(sh, c):
     assert np.array_equal(out, vectors()[c["name"] + "_out"])
 
 
+# m >= 7: host-side setup; m in {2, 4, 5, 6}: the device setup (Gauss-Jordan over the searched
+# tables) writing into the staging workspace, rows placed by the host; B = 1000 and
+# 520 are no compile-time shape (tile kernels), B = 96 is below the tile kernels (generic path).
 @pytest.mark.parametrize("k,m,B", [(200, 32, 1400), (64, 16, 1400), (150, 40, 1352), (28, 8, 256),
-                                   (100, 20, 512), (190, 66, 1336), (12, 7, 64)])
+                                   (100, 20, 512), (190, 66, 1336), (12, 7, 64),
+                                   (20, 2, 1400), (28, 4, 256), (40, 6, 1000), (30, 4, 96), (17, 5, 520)])
 def test_single_group_decode_random_patterns(sh, k, m, B):
     """cauchy_256_decode (host-side setup for m >= 7) on random erasure sets: e = 1..min(k, m) lost
     originals, a random subset of e recovery rows, blocks in random array order; results and rows

@@ -524,6 +524,14 @@ def shape(k, m):
     # LDS per workgroup: ring of R slots (the 2 KB per wave of store scratch aliases the ring after
     # the last step)
     slot = 8 * CW * 64 * 4
+    if blk_sub(k, m):  # BlkSrc: NG whole block images per slot (fixed_common.hpp BlkGeo)
+        sub = blk_sub(k, m)
+        nq = (((sub + 3) // 4) + 3) & ~3
+        gs = ((8 * sub) + 15) & ~15
+        while (gs // 4) % 32 != nq % 32:
+            gs += 16
+        ng = (127 + nq - 1) // nq + 1
+        slot = -(-ng * gs // 1024) * 1024
     rmax = int(os.environ.get("SH_RING_MAX", "19" if rbytes <= 65536 else "16"))
     R = int(os.environ.get("SH_RING", str(max(3, min(rmax, rbytes // slot, max(76 * 1024, rbytes) // slot)))))
     rows = (m + P - 1) // P
@@ -541,6 +549,22 @@ def parts_per_wg(P):
     streams per workgroup for P / PW times the input reads through L2). Default: all P."""
     pw = int(os.environ.get("SH_PW", "0")) or P
     return pw if P % pw == 0 else P
+
+
+def blk_sub(k, m):
+    """Whole-block input ring (fixed_common.hpp BlkSrc) for B = 8 * SH_BLK, A/B switch: the
+    kernel then serves that block size only. 0 = the sub-block-row gather (Src)."""
+    return int(os.environ.get("SH_BLK", "0"))
+
+
+def split_tiles(mode, k, P, pers):
+    """Split-tile programs (fixed_common.hpp RowSink "Split tiles": the launch's last tiles run
+    as two half-step workgroups combined in-launch), A/B switch SH_SPLIT_GEN=1: bit-exact but no
+    faster (profiles/r06/ab_runs.txt block 2), and the half programs triple the generated code
+    and the build time, so the product generates none."""
+    if os.environ.get("SH_SPLIT_GEN", "0") != "1" or pers or RINIT or INTERLEAVE or stream_mode(P):
+        return False
+    return k >= 16
 
 
 PERSIST = os.environ.get("SH_PERSIST", "0") == "1"
@@ -591,21 +615,31 @@ def gen_config(k, m):
            ""]
     KP = (k + 3) & ~3
     pers = {mode: persistent(mode, P, R) for mode in ("enc", "dec")}
+    split = {mode: split_tiles(mode, k, P, pers[mode]) for mode in ("enc", "dec")}
     for mode in ("enc", "dec"):
         rinit = mode == "dec" and RINIT and not pers[mode]
         steps = [("c", x) for x in range(k)] + ([("r", y) for y in range(m)] if mode == "dec" and not rinit else [])
         if INTERLEAVE and not pers[mode] and not rinit and len(parts) > 1:
             out.extend(interleaved_function(name, mode, k, rows, parts, R, sync, steps, KP))
+            out.extend(["template <class Src, class Snk>",
+                        f"__device__ __forceinline__ void run_{name}_{mode}_half(int half, int part, const Src &src, const Snk &sink) {{",
+                        f"    run_{name}_{mode}(part, src, sink);", "}", ""])
             continue
-        for p, (y0, y1) in enumerate(parts):
+        nrmax = max(b - a for a, b in parts)
+
+        def body_fn(fname, p, y0, y1, sub_steps, split_half=None, step0=0):
+            """One part's straight-line function over sub_steps; split_half: the epilogue stores a
+            partial and the second arriving half combines (RowSink "Split tiles")."""
             # epilogue stores per wave: two 16-byte pieces per row of its part (RowSink::row)
             npf = R - 2 * P if pers[mode] else 0
-            body = Body(k, rows, y0, y1, max(b - a for a, b in parts), part=p).emit(R, sync, steps, KP, npf=npf,
-                                                                            st=2 * (y1 - y0))
+            body = Body(k, rows, y0, y1, nrmax, part=p).emit(R, sync, sub_steps, KP, npf=npf,
+                                                             st=2 * (y1 - y0))
             nr = y1 - y0
             out.append(f"template <class Src, class Snk>")
-            out.append(f"__device__ __forceinline__ void run_{name}_{mode}_p{p}(const Src &src, const Snk &sink) {{")
+            out.append(f"__device__ __forceinline__ void {fname}(const Src &src, const Snk &sink) {{")
             out.append(f"    uint32_t acc[{nr}][8];")
+            if step0:
+                out.append(f"    src.set_step0({step0});  // encode: this half's first input block")
             # opaque zeros: a constant 0 would be folded into the first step, whose pinned results
             # then need register copies of shared table entries (AGPR spills at k=200).
             if rinit:
@@ -614,12 +648,11 @@ def gen_config(k, m):
                 out.append(f"    for (int y = 0; y < {nr}; ++y) for (int b = 0; b < 8; ++b) ZERO(acc[y][b]);")
             out.append(body)
             out.append("    __builtin_amdgcn_sched_barrier(0);")
-            out.append(f"    // epilogue: store rows {y0}..{y1 - 1}")
+            out.append(f"    // epilogue: store rows {y0}..{y1 - 1}" + (" (partial of a split tile)" if split_half is not None else ""))
             out.append("    src.release();  // the store scratch aliases the ring")
             if pers[mode]:
                 out.append(f"    src.prefetch_next({R - 2 * P});  // the next tile's first steps")
             out.append("    sink.prepare();")
-            nrmax = max(b - a for a, b in parts)
             for yi in range(nrmax):  # every part joins the same number of row barriers
                 out.append("    __builtin_amdgcn_sched_barrier(0);")
                 if yi >= nr:
@@ -628,10 +661,37 @@ def gen_config(k, m):
                     out.append(f"    asm volatile(\"\" :: " + ", ".join(f'"v"(acc[{yi}][{b}])' for b in range(8)) + ");")
                 elif "nostore" in ABLATE:
                     out.append(f"    asm volatile(\"\" :: " + ", ".join(f'"v"(acc[{yi}][{b}])' for b in range(8)) + ");")
+                elif split_half is not None:
+                    out.append(f"    sink.template part_row<{yi}>({y0 + yi}, acc[{yi}]);")
                 else:
                     out.append(f"    sink.template row<{yi}>({y0 + yi}, acc[{yi}]);")
+            if split_half is not None:
+                out.append(f"    sink.combine({y0}, {nr});")
             out.append("}")
             out.append("")
+
+        for p, (y0, y1) in enumerate(parts):
+            body_fn(f"run_{name}_{mode}_p{p}", p, y0, y1, steps)
+        # Split tiles: two half-step programs per part (the steps cut at an even index, so the
+        # pair units and their XOR programs are those of the whole program)
+        n0 = (len(steps) // 2) & ~1
+        if split[mode]:
+            for h, (sub, x0) in enumerate(((steps[:n0], 0), (steps[n0:], n0 if mode == "enc" else 0))):
+                for p, (y0, y1) in enumerate(parts):
+                    body_fn(f"run_{name}_{mode}_h{h}_p{p}", p, y0, y1, sub, split_half=h, step0=x0)
+        out.append(f"template <class Src, class Snk>")
+        out.append(f"__device__ __forceinline__ void run_{name}_{mode}_half(int half, int part, const Src &src, const Snk &sink) {{")
+        if split[mode]:
+            for h in (0, 1):
+                out.append(f"    {'if' if h == 0 else 'else if'} (half == {h}) {{")
+                for p in range(len(parts)):
+                    kw = "if" if p == 0 else "else if"
+                    out.append(f"        {kw} (part == {p}) run_{name}_{mode}_h{h}_p{p}(src, sink);")
+                out.append("    }")
+        else:  # never launched with split tiles (FIXED_KERNEL SPLIT = 0)
+            out.append(f"    run_{name}_{mode}(part, src, sink);")
+        out.append("}")
+        out.append("")
         out.append(f"template <class Src, class Snk>")
         out.append(f"__device__ __forceinline__ void run_{name}_{mode}(int part, const Src &src, const Snk &sink) {{")
         if "samecode" in ABLATE:  # timing only: every part-wave runs part 0's code (one code stream)
@@ -660,7 +720,7 @@ def gen_config(k, m):
                     + (f"FIXED_KERNEL_PERSISTENT({name}, {k}, {m}, {P}, {CW}, {R}, {minw}, {mode}, {dec})\n" if pers[mode] else
                        f"FIXED_KERNEL({name}, {k}, {m}, {P}, {CW}, {R}, {minw}, {mode}, {dec}, "
                        f"{'false' if 'nodma' in ABLATE else 'true'}, {'true' if stream_mode(P) else 'false'}, "
-                       f"{parts_per_wg(P)})\n"))
+                       f"{parts_per_wg(P)}, {blk_sub(k, m)}, {1 if split[mode] else 0})\n"))
         paths.append(path)
     return paths
 

@@ -15,6 +15,11 @@ for round in 1 2; do
     [ "${PIPESTATUS[0]}" = 0 ] || exit 1
   done
 done
+for v in $(echo "$1" | tr , ' '); do
+  printf "%-10s " "$v"
+  SH_LIB_PATH=$(lib "$v") timeout -k 10 120 python tools/run_ops.py --op both --iters 1 --digest 2>&1 | grep digest
+  [ "${PIPESTATUS[0]}" = 0 ] || exit 1
+done
 [ "${PMC:-1}" = 0 ] && exit 0
 i=0
 for v in $(echo "$1" | tr , ' '); do

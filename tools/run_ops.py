@@ -23,6 +23,8 @@ def main():
     p.add_argument("--erasures", type=int, default=32)
     p.add_argument("--concurrent", action="store_true", help="encode and decode on two streams at once")
     p.add_argument("--zero", action="store_true", help="all-zero data blocks (data-dependent power / DVFS check)")
+    p.add_argument("--digest", action="store_true",
+                   help="print SHA-256 digests of the recovery blocks and the decoded blocks (variant parity)")
     a = p.parse_args()
     import torch
     import shorthair_amd as sh
@@ -87,6 +89,17 @@ def main():
         torch.cuda.synchronize()
         te += ev[0].elapsed_time(ev[1])
         td += ev[1].elapsed_time(ev[2])
+    if a.digest:
+        import hashlib
+        torch.cuda.synchronize()
+        dig = {"recovery": hashlib.sha256(rec.cpu().numpy().tobytes()).hexdigest()[:16]}
+        if a.op in ("decode", "both"):
+            # the decoded blocks must equal the erased originals (device round trip)
+            lost = [[x for x in range(k) if x not in set(rows[g].tolist())] for g in range(min(G, 64))]
+            ok = all(torch.equal(out[g, :len(l)].cpu(), data[g, l].cpu()) for g, l in enumerate(lost) if l)
+            dig["decoded"] = hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest()[:16]
+            dig["roundtrip_ok"] = ok
+        print("digest", dig)
     enc_b = G * (k + m) * B
     dec_b = G * (k + a.erasures) * B
     print(f"{os.path.basename(sh.LIB_PATH)} {a.op}: encode {te / a.iters:.3f} ms ({enc_b / (te / a.iters) / 1e9:.0f} GB/s)"
