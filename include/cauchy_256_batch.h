@@ -93,7 +93,9 @@ int cauchy_256_sync(void *stream);
  * the compile-time path records HIP events on its stream around its three kernels (the last n
  * decodes are kept; nothing synchronises while recording; n = 0 turns it off).
  * profile_read waits for them and returns ms[0..2] = mean setup, stage A and stage B times and
- * the number of decodes averaged (-1: none recorded). */
+ * the number of decodes averaged (-1: none recorded). cauchy_256_profile(-n) records only the two
+ * events around stage A (the headline's dominant kernel) of the last n decodes: ms[1] is then its
+ * mean time and ms[0], ms[2] are -1. */
 int cauchy_256_profile(int capacity);
 int cauchy_256_profile_read(float *ms);
 

@@ -200,7 +200,8 @@ def sync(stream=None):
 
 
 def profile(capacity=64):
-    """Record HIP events around the stages of the next `capacity` batched decodes (0: off)."""
+    """Record HIP events around the stages of the next `capacity` batched decodes (0: off;
+    negative: only the two events around stage A of the next -capacity decodes)."""
     return _check(lib.cauchy_256_profile(int(capacity)), "profile")
 
 

@@ -96,6 +96,21 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wg_rsrc(const uint8_t *base, l
     return make_rsrc(base + start, static_cast<uint32_t>(n));
 }
 
+// XCD-aware tile order. Workgroups are dealt round-robin over the 8 XCDs (block b -> XCD b % 8;
+// a speed assumption, never a correctness one). Adjacent column tiles usually split a group, so
+// both read the same 128-byte lines at their shared edge; giving them blocks b and b + 8 puts
+// them on one XCD at about the same time, and the second read hits that XCD's L2 instead of
+// going to HBM again (measured: 29% over-fetch on the staging microbenchmark without it; a
+// persistent variant that walked each workgroup's own group range tile by tile re-read those
+// lines from memory: +30% FETCH_SIZE, 0.94 vs 0.75 ms, round 2). Bijective map of block b in
+// [0, n) to a tile: XCD i gets the contiguous tile range [start_i, start_i + count_i),
+// count_i = n/8 (+1 for the first n%8 XCDs).
+__device__ __forceinline__ int xcd_tile(int b, int n) {
+    const int q = n >> 3, r = n & 7;
+    const int x = b & 7, i = b >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
 // Compile-time shape of one kernel instance.
 // DMA_ = false only in measurement builds (tools/gen_fixed_kernels.py SH_GEN_ABLATE=nodma).
 // PW_ = parts per workgroup (default all P): with PW < P the P parts of a tile run in H = P / PW
@@ -187,6 +202,7 @@ struct Src {
     // encode: byte offset of step 0's block (the second half of a split tile starts at block x0)
     mutable uint32_t boff = 0;
     __device__ __forceinline__ void set_step0(int x0) const { boff = static_cast<uint32_t>(x0) * B; }
+    int pf_stride = 0;        // FixedArgs::pf_stride (l2_prefetch)
 
     __device__ __forceinline__ static void chunk_src(const Geometry &geo, long long in_gstride_, const WGInfo &w,
                                                      uint32_t (&db)[S::DPW], int (&gl)[S::DPW]) {
@@ -223,6 +239,7 @@ struct Src {
         pos_g = a.pos;
         rpos_g = a.rpos;
         lgl = w.gl;
+        pf_stride = a.pf_stride;
         lbase = w.valid ? static_cast<uint32_t>(w.gl) * static_cast<uint32_t>(a.in_gstride) + col_off(w.q, geo) : OOR;
     }
 
@@ -321,6 +338,54 @@ struct Src {
                 }
             }
         }
+    }
+
+    // Encode, generator switch SH_L2PF=N (A/B): at the start of the epilogue, touch the first N
+    // steps of the tile that workgroup blockIdx.x + pf_stride codes (the one about to take a slot
+    // on this XCD when every workgroup takes as long: pf_stride = the launch's slots) with plain
+    // dword loads, so its ring fill hits this XCD's L2 instead of waiting on HBM (the lab's first
+    // ring wait: 9.2 us of a 109 us tile). The loads' results are never used; the generated
+    // epilogue ends with a vmcnt wait that leaves only its own stores outstanding.
+    // The loads' values are kept live until l2_done (an empty asm using them), so the compiler
+    // places its own counted wait for them there, after the epilogue's stores are issued.
+    template <int N>
+    struct L2Pf {
+        uint32_t v[N * S::DPW];
+    };
+    template <int N>
+    __device__ __forceinline__ L2Pf<N> l2_prefetch() const {
+        L2Pf<N> pf;
+#pragma unroll
+        for (int i = 0; i < N * S::DPW; ++i) pf.v[i] = 0;
+        if (DEC || pf_stride <= 0) return pf;
+        const int nb = static_cast<int>(blockIdx.x) + pf_stride;
+        if (nb >= static_cast<int>(gridDim.x)) return pf;
+        const long long gstride = static_cast<long long>(S::K) * B;
+        const long long cols = static_cast<long long>(groups) * nq;
+        const WGInfo w = tile_info<S>(nq, static_cast<long long>(xcd_tile(nb, gridDim.x)) * S::COLS, 0, cols);
+        const __amdgpu_buffer_rsrc_t r = wg_rsrc(in_ptr, gstride * groups, gstride, w.g_first);
+        Geometry g;
+        g.B = static_cast<int>(B);
+        g.sub = static_cast<int>(sub);
+        g.nq = nq;
+        g.tail = 4;
+        uint32_t db[S::DPW];
+        int gl[S::DPW];
+        chunk_src(g, gstride, w, db, gl);
+#pragma unroll
+        for (int t = 0; t < N; ++t) {
+#pragma unroll
+            for (int j = 0; j < S::DPW; ++j) {
+                if (S::NDMA % S::NW != 0 && wave * S::DPW + j >= S::NDMA) break;  // uniform
+                pf.v[t * S::DPW + j] = __builtin_amdgcn_raw_buffer_load_b32(r, db[j], static_cast<uint32_t>(t) * B, 0);
+            }
+        }
+        return pf;
+    }
+    template <int N>
+    __device__ __forceinline__ static void l2_done(const L2Pf<N> &pf) {
+#pragma unroll
+        for (int i = 0; i < N * S::DPW; ++i) asm volatile("" ::"v"(pf.v[i]));
     }
 
     // Persistent encode, a prefetched tile: every wave has finished reading the previous tile's
@@ -891,20 +956,6 @@ __device__ __forceinline__ int kernel_prologue(const FixedArgs &a, uint8_t *lds,
     return part;  // the generated body issues the ring's first DMAs
 }
 
-// XCD-aware tile order. Workgroups are dealt round-robin over the 8 XCDs (block b -> XCD b % 8;
-// a speed assumption, never a correctness one). Adjacent column tiles usually split a group, so
-// both read the same 128-byte lines at their shared edge; giving them blocks b and b + 8 puts
-// them on one XCD at about the same time, and the second read hits that XCD's L2 instead of
-// going to HBM again (measured: 29% over-fetch on the staging microbenchmark without it; a
-// persistent variant that walked each workgroup's own group range tile by tile re-read those
-// lines from memory: +30% FETCH_SIZE, 0.94 vs 0.75 ms, round 2). Bijective map of block b in
-// [0, n) to a tile: XCD i gets the contiguous tile range [start_i, start_i + count_i),
-// count_i = n/8 (+1 for the first n%8 XCDs).
-__device__ __forceinline__ int xcd_tile(int b, int n) {
-    const int q = n >> 3, r = n & 7;
-    const int x = b & 7, i = b >> 3;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
-}
 
 // Persistent encode workgroups: two per CU (the LDS ring and the registers allow two), each
 // walking tiles v = blockIdx.x + i * grid in xcd_tile order (grid % 8 == 0, so every tile of a
@@ -977,9 +1028,9 @@ bool tag_is_module(const char *tag);
 // of the last tiles, so the grid drains in half-tile tasks; every tile when all halves fit one
 // round. A multiple of 8 (split_tile_of), at most what the caller's scratch holds, 0 below 8.
 // SH_SPLIT (measurement builds only) forces the count (0: no split).
+// Workgroups of this kernel resident at once on the device (occupancy x CUs), cached.
 template <class S, bool DEC>
-inline int split_count(const FixedArgs &a, int ntiles, void (*kern)(FixedArgs), size_t lds) {
-    if (!a.split_part || !a.split_cnt || S::H != 1) return 0;
+inline int launch_slots(void (*kern)(FixedArgs), size_t lds) {
     static const int slots = [&] {
         int per_cu = 0, d = 0, cus = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, S::NT, lds) != hipSuccess || per_cu < 1) per_cu = 1;
@@ -987,6 +1038,13 @@ inline int split_count(const FixedArgs &a, int ntiles, void (*kern)(FixedArgs), 
             cus = 256;
         return per_cu * (cus > 0 ? cus : 256);
     }();
+    return slots;
+}
+
+template <class S, bool DEC>
+inline int split_count(const FixedArgs &a, int ntiles, void (*kern)(FixedArgs), size_t lds) {
+    if (!a.split_part || !a.split_cnt || S::H != 1) return 0;
+    const int slots = launch_slots<S, DEC>(kern, lds);
     long long n = std::min<long long>(ntiles, slots / 2);
     if (const char *e = SH_MEASURE_ENV("SH_SPLIT")) n = std::min<long long>(ntiles, std::atoi(e));
     const long long per = 2ll * S::M * 32 * S::COLS;  // partial bytes per split tile
@@ -1010,6 +1068,7 @@ inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArg
     unsigned blocks = static_cast<unsigned>(ntiles >= 0 ? ntiles : (cols + S::COLS - 1) / S::COLS);  // one tile each
     if (S::H > 1) blocks = (blocks + 7) / 8 * 8 * S::H;  // tile_of(): H part-groups per tile
     a.nsplit = (SPLIT && !PERS && !tag_is_module(tag)) ? split_count<S, DEC>(a, static_cast<int>(blocks), kern, lds) : 0;
+    a.pf_stride = launch_slots<S, DEC>(kern, lds);
     blocks += static_cast<unsigned>(a.nsplit);  // split tiles: two workgroups each
     if (PERS) blocks = std::min<unsigned>(blocks, static_cast<unsigned>(persistent_slots()));
     if (tag) {

@@ -59,6 +59,7 @@ struct FixedArgs {
     long long split_cap;
     int split_max;            // counters available (split tiles at most)
     int nsplit;
+    int pf_stride;            // workgroup slots of the launch (L2 prefetch of a later tile, A/B)
 };
 
 }  // namespace sh

@@ -244,7 +244,7 @@ struct SetupScratch {
     uint8_t rrow[256];     // its generator row r_i = row - k
     uint8_t era[256];      // j-th erased original row E_j
     uint8_t x[256], y[256];
-    uint8_t la[256], lb[256], lx[256];  // logs mod 255
+    uint8_t la[256], lb[256];  // log a_j - log x_j and log b_i, mod 255
 };
 
 // Every wave handles its own group and synchronises only with itself: its lanes run in lockstep,
@@ -259,7 +259,9 @@ __global__ __launch_bounds__(64 * W, 8) void decode_setup(DecodeSetupArgs a, int
     const int g = blockIdx.x * W + wave;
     const int lane = threadIdx.x & 63;
     const int k = a.k, m = a.m;
-    __shared__ uint8_t s_exp[512];
+    // exp over [0, 1024): every exponent sum of the closed form's coefficients, [1, 763], without a
+    // mod-255 reduction (s_exp[i] = exp(i mod 255))
+    __shared__ uint8_t s_exp[1024];
     __shared__ uint8_t s_log[256];
     // generator data the coefficients need, staged with the tables so the per-group chain has one
     // global round trip (the rows): m <= 6 the searched rows 1..m-1, m >= 7 the Cauchy X', Y'
@@ -268,12 +270,26 @@ __global__ __launch_bounds__(64 * W, 8) void decode_setup(DecodeSetupArgs a, int
     __shared__ SetupScratch sw[W];
     SetupScratch &S = sw[wave];
 
+    // Every global load of the staging is issued before any is waited for (one round trip): the
+    // group's row bytes as dwords where aligned, four exp entries per thread.
     if (g < groups) {
         const uint8_t *rows = a.rows + static_cast<long long>(g) * a.rows_gstride;
-        for (int j = lane; j < k; j += 64) S.rows[j] = rows[j];
+        if ((k & 3) == 0 && (reinterpret_cast<uintptr_t>(rows) & 3) == 0) {
+            if (4 * lane < k)
+                *reinterpret_cast<uint32_t *>(S.rows + 4 * lane) = *reinterpret_cast<const uint32_t *>(rows + 4 * lane);
+        } else {
+            for (int j = lane; j < k; j += 64) S.rows[j] = rows[j];
+        }
     }
     S.present[lane] = 0;
-    for (int i = threadIdx.x; i < 512; i += 64 * W) s_exp[i] = a.gf_exp[i];
+    static_assert(64 * W * 4 >= 1024, "four exp entries per thread");
+    {
+        uint8_t ev[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ev[u] = a.gf_exp[(4 * threadIdx.x + u) % 255];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s_exp[4 * threadIdx.x + u] = ev[u];
+    }
     for (int i = threadIdx.x; i < 256; i += 64 * W) s_log[i] = static_cast<uint8_t>(a.gf_log[i]);
     if (m <= 6) {
         for (int i = threadIdx.x; i < (m - 1) * k; i += 64 * W) s_gen[i] = a.gen[i];
@@ -414,24 +430,27 @@ __global__ __launch_bounds__(64 * W, 8) void decode_setup(DecodeSetupArgs a, int
             S.y[t] = s_yp[S.rrow[t]];
         }
         SH_WAVE_SYNC();
-        for (int t = lane; t < e; t += 64) {
-            const int xt = S.x[t], yt = S.y[t];
-            int la = 0, lb = 0;
+        // log a_j - log x_j (items w < e, into la) and log b_i (items e <= w < 2e, into lb) on all
+        // 64 lanes: a_j's sum runs over the other set (y) and its product over its own (x), b_i's
+        // the other way round; q-loop unrolled so the lookups of several terms are in flight.
+        for (int w = lane; w < 2 * e; w += 64) {
+            const bool isa = w < e;
+            const int t = isa ? w : w - e;
+            const uint8_t *other = isa ? S.y : S.x;
+            const uint8_t *own = isa ? S.x : S.y;
+            const int me = own[t];
+            int acc = isa ? 255 * 130 - s_log[me] : 255 * 130;  // offset keeps the sum positive
+#pragma unroll 4
             for (int q = 0; q < e; ++q) {
-                la += s_log[xt ^ S.y[q]];
-                lb += s_log[S.x[q] ^ yt];
-                if (q != t) {
-                    la -= s_log[xt ^ S.x[q]];
-                    lb -= s_log[yt ^ S.y[q]];
-                }
+                acc += s_log[me ^ other[q]];
+                acc -= q != t ? s_log[me ^ own[q]] : 0;
             }
-            S.la[t] = static_cast<uint8_t>(mod255(la));
-            S.lb[t] = static_cast<uint8_t>(mod255(lb));
-            S.lx[t] = s_log[xt];
+            (isa ? S.la : S.lb)[t] = static_cast<uint8_t>(acc % 255);
         }
         SH_WAVE_SYNC();
+        // S^-1[j][i] = exp(log a_j - log x_j + log b_i - log(x_j + y_i)); index in [1, 763]
         auto coef = [&](int j, int i) -> uint32_t {
-            return s_exp[mod255(S.la[j] + S.lb[i] - S.lx[j] - s_log[S.x[j] ^ S.y[i]])];
+            return s_exp[S.la[j] + S.lb[i] + 255 - s_log[S.x[j] ^ S.y[i]]];
         };
         // Walk the output in memory order so every store instruction writes contiguous bytes,
         // the unused entries included: addresses [j/8][i][j%8] (i < e), bytes [i][j] (i < emax).
@@ -444,9 +463,18 @@ __global__ __launch_bounds__(64 * W, 8) void decode_setup(DecodeSetupArgs a, int
                     c ? a.snip_base + static_cast<uint64_t>(c) * SNIP_STRIDE : tnull;
             }
         } else {
-            for (int t = lane; t < emax * a.ldB; t += 64) {
-                const int i = t / a.ldB, j = t - i * a.ldB;
+            // t = i * ldB + j stepped by 64 without a division per entry
+            const int ldB = a.ldB, iinc = 64 / ldB, jinc = 64 - iinc * ldB, n = emax * ldB;
+            int i = lane / ldB, j = lane - i * ldB;
+#pragma unroll 4
+            for (int t = lane; t < n; t += 64) {
                 Bc[t] = static_cast<uint8_t>(i < e && j < e ? coef(j, i) : 0u);
+                j += jinc;
+                i += iinc;
+                if (j >= ldB) {
+                    j -= ldB;
+                    ++i;
+                }
             }
         }
         return;

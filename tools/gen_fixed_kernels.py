@@ -567,6 +567,9 @@ def split_tiles(mode, k, P, pers):
     return k >= 16
 
 
+# A/B switch SH_L2PF=N: encode epilogues touch the first N steps of a later tile (Src::l2_prefetch)
+L2PF = int(os.environ.get("SH_L2PF", "0"))
+
 PERSIST = os.environ.get("SH_PERSIST", "0") == "1"
 # Decode stage A, SH_RINIT=1 (measured, not the default): residual rows start as the recovery
 # blocks R_y, loaded into the accumulators in the prologue (Src::rrow) instead of m extra ring
@@ -650,6 +653,8 @@ def gen_config(k, m):
             out.append("    __builtin_amdgcn_sched_barrier(0);")
             out.append(f"    // epilogue: store rows {y0}..{y1 - 1}" + (" (partial of a split tile)" if split_half is not None else ""))
             out.append("    src.release();  // the store scratch aliases the ring")
+            if L2PF and mode == "enc" and not pers[mode] and split_half is None:
+                out.append(f"    const auto l2pf = src.template l2_prefetch<{L2PF}>();  // A/B: warm L2 for a later tile")
             if pers[mode]:
                 out.append(f"    src.prefetch_next({R - 2 * P});  // the next tile's first steps")
             out.append("    sink.prepare();")
@@ -667,6 +672,8 @@ def gen_config(k, m):
                     out.append(f"    sink.template row<{yi}>({y0 + yi}, acc[{yi}]);")
             if split_half is not None:
                 out.append(f"    sink.combine({y0}, {nr});")
+            if L2PF and mode == "enc" and not pers[mode] and split_half is None:
+                out.append("    src.l2_done(l2pf);  // the compiler's counted wait: the prefetch loads only")
             out.append("}")
             out.append("")
 
