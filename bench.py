@@ -38,6 +38,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--settle-steps", type=int, default=40,
+                   help="untimed steps before the warm-up: the GPU's power management needs ~20-30 "
+                        "steps of sustained load after idle to settle its clock (tools/ramp_probe.py)")
     p.add_argument("--k", type=int, default=200)
     p.add_argument("--m", type=int, default=32)
     p.add_argument("--block", type=int, default=1400)
@@ -633,9 +636,8 @@ def main():
             evs[2].record(stream)
         assert rc1 == 0 and rc2 == 0
 
-    # correctness guard on the timed buffers (after the first warm-up step, and again after the
-    # timed steps): the recovered blocks equal the erased originals. The host check sits after the
-    # FIRST warm-up step, so the remaining W - 1 run right before the timed ones with no idle gap.
+    # correctness guard on the timed buffers (after the first settle step, and again after the
+    # timed steps): the recovered blocks equal the erased originals.
     def check():
         cnt = dec_cnt.cpu().numpy()
         assert np.array_equal(cnt, es)
@@ -643,11 +645,17 @@ def main():
         ok = torch.equal(dec_out, enc_in[g_chk, dec_rows.long()]) if args.erasures == emax else True
         assert ok, "decode output mismatch"
 
+    # Settle: the MI355X's power management needs ~20-30 steps (~40 ms) of sustained load after
+    # any idle before the step time is steady (tools/ramp_probe.py, profiles/r06/ab_runs.txt block
+    # 5: steps 0-9 from idle 1.86 ms, 10-19 1.67, 20+ 1.62-1.63). These steps are untimed like
+    # the W warm-up steps that follow them, and reported in the line ("settle_steps").
+    step()
+    torch.cuda.synchronize()
+    check()
+    for _ in range(max(0, args.settle_steps - 1)):
+        step()
     for i in range(args.warmup):
         step()
-        if i == 0:
-            torch.cuda.synchronize()
-            check()
 
     # ---- timed region ----
     # Only the two HIP events around the dominant kernel (decode stage A, for the roofline) are
@@ -741,6 +749,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_steps": args.settle_steps,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
             "scaling": "strong" if args.total_groups else "weak",
