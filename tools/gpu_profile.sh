@@ -28,7 +28,7 @@ pmc sq GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_A
 python3 tools/pmc_summary.py "$OUT/sq" > "$OUT/sq.txt"
 python3 tools/traffic_json.py "$OUT" > "$OUT/traffic.json" || exit 1
 # bench.py reads profiles/*/traffic*.json (matched by the library hash): the run below sees it
-PROFDIR=${PROFDIR:-profiles/r05}; mkdir -p $PROFDIR && cp "$OUT/traffic.json" "$PROFDIR/traffic_$TAG.json"
+PROFDIR=${PROFDIR:-profiles/r06}; mkdir -p $PROFDIR && cp "$OUT/traffic.json" "$PROFDIR/traffic_$TAG.json"
 if [ -n "${IFETCH:-}" ]; then  # e.g. IFETCH="SQC_ICACHE_REQ SQC_ICACHE_MISSES" (names from --list-avail)
   pmc ifetch $IFETCH || exit 1
   python3 tools/pmc_summary.py "$OUT/ifetch" > "$OUT/ifetch.txt"
