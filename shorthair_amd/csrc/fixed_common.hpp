@@ -918,6 +918,35 @@ struct RowSink {
     __device__ __forceinline__ void pad() const {
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
+
+    // Row pairs (generator switch SH_ROW_PAIRS=1, A/B): rows 2i and 2i+1 share one barrier --
+    // both images written, one barrier, then the four pieces read and stored -- so a part's 8
+    // rows take 4 epilogue barriers instead of 8. Images [pair parity][row of the pair][PW][IMG]
+    // (4 * PW * IMG bytes: the whole 64 KB ring at P = 4). LAST: the part's largest row count
+    // ends on this row (an even row then stores alone).
+    template <int YI, bool LAST>
+    __device__ __forceinline__ void row2(int y, const uint32_t (&w)[8]) const {
+        static_assert(4 * S::PW * S::IMG <= S::R * S::SLOT, "row-pair images must fit inside the ring");
+        uint8_t *im = img + (((YI >> 1) & 1) * 2 + (YI & 1)) * S::PW * S::IMG;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) *reinterpret_cast<uint32_t *>(im + b * S::ROWB + wofs) = w[b];
+        if ((YI & 1) == 0 && !LAST) return;  // the pair's second row brings the barrier
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if ((YI & 1) == 1) {
+            const uint8_t *im0 = im - S::PW * S::IMG;
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                __builtin_amdgcn_raw_buffer_store_b128(piece(im0, h), rsrc, gdst[h], static_cast<uint32_t>(y - 1) * B, SH_STORE_AUX);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            __builtin_amdgcn_raw_buffer_store_b128(piece(im, h), rsrc, gdst[h], static_cast<uint32_t>(y) * B, SH_STORE_AUX);
+    }
+    template <int YI, bool LAST>
+    __device__ __forceinline__ void pad2() const {
+        if ((YI & 1) == 0 && !LAST) return;
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
 };
 
 // Sets up src/sink for the tile starting at column col0 (columns outside [lo, hi) are idle

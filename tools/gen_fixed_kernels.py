@@ -567,6 +567,8 @@ def split_tiles(mode, k, P, pers):
     return k >= 16
 
 
+# A/B switch SH_ROW_PAIRS=1: two rows per epilogue barrier (RowSink::row2)
+ROW_PAIRS = os.environ.get("SH_ROW_PAIRS", "0") == "1"
 # A/B switch SH_L2PF=N: encode epilogues touch the first N steps of a later tile (Src::l2_prefetch)
 L2PF = int(os.environ.get("SH_L2PF", "0"))
 
@@ -658,9 +660,15 @@ def gen_config(k, m):
             if pers[mode]:
                 out.append(f"    src.prefetch_next({R - 2 * P});  // the next tile's first steps")
             out.append("    sink.prepare();")
+            # row pairs (A/B switch): not with the persistent form (its images sit in the ring's
+            # top 2P slots) nor the split tiles' partial rows
+            pairs = ROW_PAIRS and not pers[mode] and split_half is None and 4 * parts_per_wg(P) <= R
             for yi in range(nrmax):  # every part joins the same number of row barriers
                 out.append("    __builtin_amdgcn_sched_barrier(0);")
-                if yi >= nr:
+                last = "true" if yi == nrmax - 1 else "false"
+                if yi >= nr and pairs:
+                    out.append(f"    sink.template pad2<{yi}, {last}>();")
+                elif yi >= nr:
                     out.append(f"    sink.template pad<{yi}>();")
                 elif "halfstore" in ABLATE and p >= len(parts) // 2:
                     out.append(f"    asm volatile(\"\" :: " + ", ".join(f'"v"(acc[{yi}][{b}])' for b in range(8)) + ");")
@@ -668,6 +676,8 @@ def gen_config(k, m):
                     out.append(f"    asm volatile(\"\" :: " + ", ".join(f'"v"(acc[{yi}][{b}])' for b in range(8)) + ");")
                 elif split_half is not None:
                     out.append(f"    sink.template part_row<{yi}>({y0 + yi}, acc[{yi}]);")
+                elif pairs:
+                    out.append(f"    sink.template row2<{yi}, {last}>({y0 + yi}, acc[{yi}]);")
                 else:
                     out.append(f"    sink.template row<{yi}>({y0 + yi}, acc[{yi}]);")
             if split_half is not None:
