@@ -17,6 +17,7 @@
 #include <stdint.h>
 
 #include "kernels.hpp"
+#include "measure.hpp"
 
 namespace sh {
 
@@ -545,6 +546,209 @@ __global__ __launch_bounds__(64 * W, 8) void decode_setup(DecodeSetupArgs a, int
         if (el[h] && c[h] >= e) put(r[h], c[h] - e, v[h]);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Decode setup for the searched generators (m <= 6) in fixed-kernel mode: eight lanes per group,
+// eight groups per wave. Same outputs as decode_setup above; there a wave spends a chain of
+// dependent LDS / global round trips on one group with e <= 6, so a (28,4,256) batch of 209,263
+// groups ran ~25 rounds of resident waves (0.215 ms of a 0.743 ms decode). Here a wave carries 8
+// groups through the same chain and a row of the e x 2e Gauss-Jordan lives in one lane.
+// ---------------------------------------------------------------------------------------------
+struct SmallScratch {
+    uint8_t rows[256];
+    uint8_t pos[256];       // pos table image (round4(k) <= 252 entries)
+    uint32_t present[8];    // bitmap of row values
+    uint8_t rpos[8];        // rpos table image (round4(m) <= 8 entries)
+    uint8_t rec[8], rrow[8], era[8];
+};
+
+// One Gauss-Jordan row of up to 12 bytes in three registers (byte c at bits 8 (c & 3) of word
+// c >> 2); every index goes through selects, so no array is ever placed in scratch.
+struct Row12 {
+    uint32_t w0 = 0u, w1 = 0u, w2 = 0u;
+    __device__ uint32_t byte(int c) const {
+        const uint32_t v = c < 4 ? w0 : (c < 8 ? w1 : w2);
+        return (v >> (8 * (c & 3))) & 0xFFu;
+    }
+    __device__ void or_byte(int c, uint32_t v) {
+        const uint32_t x = v << (8 * (c & 3));
+        if (c < 4) w0 |= x;
+        else if (c < 8) w1 |= x;
+        else w2 |= x;
+    }
+    __device__ Row12 from_lane(int src) const {
+        Row12 r;
+        r.w0 = __shfl(w0, src);
+        r.w1 = __shfl(w1, src);
+        r.w2 = __shfl(w2, src);
+        return r;
+    }
+    __device__ Row12 operator^(const Row12 &o) const {
+        Row12 r;
+        r.w0 = w0 ^ o.w0;
+        r.w1 = w1 ^ o.w1;
+        r.w2 = w2 ^ o.w2;
+        return r;
+    }
+};
+
+template <int W>
+__global__ __launch_bounds__(64 * W, 8) void decode_setup_small(DecodeSetupArgs a, int groups) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int sub = lane >> 3, l = lane & 7, gb = 8 * sub;  // gb: first lane of this group
+    const int g = (blockIdx.x * W + wave) * 8 + sub;
+    const int k = a.k, m = a.m;
+    __shared__ uint8_t s_exp[512];
+    __shared__ uint8_t s_log[256];
+    __shared__ uint8_t s_gen[5 * 256];
+    __shared__ SmallScratch sw[8 * W];
+    SmallScratch &S = sw[8 * wave + sub];
+    const bool live = g < groups;
+    if (live) {  // the group's row bytes (all loads in flight together), present bitmap cleared
+        const uint8_t *rows = a.rows + static_cast<long long>(g) * a.rows_gstride;
+        for (int j = l; j < k; j += 8) S.rows[j] = rows[j];
+        S.present[l] = 0;
+    }
+    for (int i = threadIdx.x; i < 512; i += 64 * W) s_exp[i] = a.gf_exp[i];
+    for (int i = threadIdx.x; i < 256; i += 64 * W) s_log[i] = static_cast<uint8_t>(a.gf_log[i]);
+    for (int i = threadIdx.x; i < (m - 1) * k; i += 64 * W) s_gen[i] = a.gen[i];
+    __syncthreads();  // the only workgroup barrier: groups below may finish independently
+    if (!live) return;
+    // group-local ballot: bit l of the result = predicate of lane l of this group
+    auto gballot = [&](bool p) { return static_cast<unsigned>((__ballot(p) >> gb) & 0xFFull); };
+    auto fail = [&]() {
+        if (l == 0) {
+            a.e_out[g] = -1;
+            if (a.errors) atomicAdd(a.errors, 1);
+        }
+    };
+    // A row listed twice, or a recovery row past the generator, is outside the reference's
+    // contract (decode_setup above): the group is left untouched and reported.
+    bool bad = false;
+    for (int j = l; j < k; j += 8) {
+        const int row = S.rows[j];
+        const uint32_t bit = 1u << (row & 31);
+        bad |= (atomicOr(&S.present[row >> 5], bit) & bit) != 0u || row >= k + m;
+    }
+    if (gballot(bad)) {
+        fail();
+        return;
+    }
+    SH_WAVE_SYNC();
+    // Ordered compaction, eight entries per step: recovery blocks in array order (unique rows in
+    // [k, k+m): at most m of them), erased originals ascending (the first 8 are kept; e <= m).
+    int nrec = 0, nera = 0;
+    for (int base = 0; base < k; base += 8) {
+        const int j = base + l;
+        const int row = j < k ? S.rows[j] : 0;
+        const bool isrec = j < k && row >= k;
+        const bool miss = j < k && ((S.present[j >> 5] >> (j & 31)) & 1u) == 0u;
+        const unsigned mr = gballot(isrec), me = gballot(miss);
+        const unsigned below = (1u << l) - 1u;
+        if (isrec) {
+            const int p = nrec + __popc(mr & below);
+            S.rec[p] = static_cast<uint8_t>(j);
+            S.rrow[p] = static_cast<uint8_t>(row - k);
+        }
+        if (miss) {
+            const int p = nera + __popc(me & below);
+            if (p < 8) S.era[p] = static_cast<uint8_t>(j);
+        }
+        nrec += __popc(mr);
+        nera += __popc(me);
+    }
+    // position tables, assembled in LDS and stored as dwords
+    const int KP = (k + 3) & ~3, MP = (m + 3) & ~3;
+    for (int x = l; x < KP; x += 8) S.pos[x] = 0xFF;
+    S.rpos[l] = 0xFF;
+    SH_WAVE_SYNC();
+    for (int j = l; j < k; j += 8) {
+        const int row = S.rows[j];
+        if (row < k) S.pos[row] = static_cast<uint8_t>(j);
+        else S.rpos[row - k] = static_cast<uint8_t>(j);
+    }
+    SH_WAVE_SYNC();
+    {
+        uint32_t *pos = reinterpret_cast<uint32_t *>(a.pos + static_cast<long long>(g) * KP);
+        for (int t = l; t < KP / 4; t += 8) pos[t] = reinterpret_cast<const uint32_t *>(S.pos)[t];
+        uint32_t *rpos = reinterpret_cast<uint32_t *>(a.rpos + static_cast<long long>(g) * MP);
+        if (l < MP / 4) rpos[l] = reinterpret_cast<const uint32_t *>(S.rpos)[l];
+    }
+    const int e = nrec;
+    if (l == 0) a.e_out[g] = e;
+    if (e == 0) return;
+    if (nera < e) {  // unreachable with unique rows; kept as in decode_setup
+        fail();
+        return;
+    }
+    const int emax = a.emax;
+    if (l < e) {
+        a.rec_idx[static_cast<long long>(g) * emax + l] = S.rec[l];
+        a.erasures[static_cast<long long>(g) * emax + l] = S.era[l];
+        a.rrow[static_cast<long long>(g) * a.ldR + l] = S.rrow[l];
+    }
+    uint8_t *Bc = a.targets ? nullptr : a.coefB + static_cast<long long>(g) * a.coefB_gstride;
+    uint64_t *Tg = a.targets ? a.targets + static_cast<long long>(g) * emax * a.ldB : nullptr;
+    const uint64_t tnull = a.snip_base + static_cast<uint64_t>(SNIP_NULL) * SNIP_STRIDE;
+    if (Tg) {  // null snippet for the unused outputs j in [e, ldB)
+        const int pad = a.ldB - e;
+        for (int t = l; t < e * pad; t += 8) {
+            const int i = t / pad, j = e + (t - i * pad);
+            Tg[(static_cast<long long>(j >> 3) * emax + i) * 8 + (j & 7)] = tnull;
+        }
+    } else {
+        for (int t = l; t < emax * a.ldB; t += 8) Bc[t] = 0;
+    }
+
+    // Gauss-Jordan on [S | I], S[i][j] = C[r_i][E_j]: lane l < e holds row l (2e <= 12 bytes).
+    Row12 u;
+    if (l < e) {
+        const int r = S.rrow[l];
+#pragma unroll
+        for (int c = 0; c < 12; ++c) {
+            uint32_t v = 0u;
+            if (c < e) v = r == 0 ? 1u : s_gen[(r - 1) * k + S.era[c]];
+            else if (c < 2 * e) v = c - e == l ? 1u : 0u;
+            u.or_byte(c, v);
+        }
+    }
+    for (int col = 0; col < e; ++col) {
+        const unsigned cand = gballot(l >= col && l < e && u.byte(col) != 0u);
+        if (cand == 0u) {  // singular: impossible for an MDS submatrix
+            fail();
+            return;
+        }
+        const int p = __ffs(cand) - 1;  // first candidate row (group-uniform)
+        if (p != col) u = u.from_lane(gb + (l == col ? p : (l == p ? col : l)));
+        const Row12 pu = u.from_lane(gb + col);
+        // row l <- row l + f * pinv * pivot row (f = its pivot-column entry); the pivot row itself
+        // <- pinv * pivot row. Exponent sums below 2 * 255: no reduction for the exp lookup.
+        const int lp = 255 - s_log[pu.byte(col)];  // log of the pivot's inverse
+        const uint32_t f = u.byte(col);
+        const bool me = l == col;
+        int lf = me ? lp : lp + s_log[f];
+        lf = lf >= 255 ? lf - 255 : lf;
+        if (l < e && (me || f != 0u)) {
+            Row12 nu;
+#pragma unroll
+            for (int c = 0; c < 12; ++c) {
+                const uint32_t b = pu.byte(c);
+                nu.or_byte(c, b ? s_exp[lf + s_log[b]] : 0u);
+            }
+            u = me ? nu : u ^ nu;
+        }
+    }
+    // lane j holds row j of S^-1 in columns e .. 2e-1
+    if (l < e) {
+        for (int i = 0; i < e; ++i) {
+            const uint32_t v = u.byte(e + i);
+            if (Tg)
+                Tg[static_cast<long long>(i) * 8 + l] = v ? a.snip_base + static_cast<uint64_t>(v) * SNIP_STRIDE : tnull;
+            else
+                Bc[static_cast<long long>(i) * a.ldB + l] = static_cast<uint8_t>(v);
+        }
+    }
+}
+
 // In-place finish of decode: recovered erasure l (dense scratch) goes to the l-th recovery block
 // of the group, whose row becomes erasure l. One thread per 4-byte word of the recovered data.
 __global__ __launch_bounds__(256) void scatter_recovered(ScatterArgs a) {
@@ -700,6 +904,13 @@ hipError_t launch_copy_first(const uint8_t *in, long long in_gstride, uint8_t *o
 
 hipError_t launch_decode_setup(const DecodeSetupArgs &a, int groups, hipStream_t stream) {
     constexpr int W = 4;
+    // measurement builds: SH_SETUP_WAVE=1 runs the one-wave-per-group kernel for every shape
+    static const bool wave_only = measure_int(SH_MEASURE_ENV("SH_SETUP_WAVE"), 0) != 0;
+    if (a.coefA == nullptr && a.m <= 6 && a.k <= 250 && !wave_only) {
+        hipLaunchKernelGGL(decode_setup_small<W>, dim3((groups + 8 * W - 1) / (8 * W)), dim3(64 * W), 0, stream,
+                           a, groups);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(decode_setup<W>, dim3((groups + W - 1) / W), dim3(64 * W), 0, stream, a, groups);
     return hipGetLastError();
 }

@@ -414,6 +414,74 @@ def test_decode_two_streams_concurrent(sh):
         assert torch.equal(out[mask], truth[mask])
 
 
+@pytest.mark.parametrize("k,m,B", [(28, 4, 256), (28, 4, 1400), (20, 6, 1400), (40, 2, 512),
+                                   (250, 6, 1400), (33, 3, 256)])
+def test_searched_table_setup_mixed_groups(sh, k, m, B):
+    """m <= 6 setup (decode_setup_small: eight groups per wave, eight lanes per group) with every
+    kind of group side by side in one wave: random e = 1..m in random array order, nothing erased
+    (e = 0), a recovery row listed twice, a row past the generator. Counts, recovered blocks and
+    rows against the oracle; the malformed groups are counted and left untouched."""
+    import torch
+    ora = po.oracle()
+    rng = np.random.default_rng(k * 31 + m * 7 + B)
+    G = 77
+    data = rng.integers(0, 256, (G, k, B), dtype=np.uint8)
+    rows = np.zeros((G, k), np.uint8)
+    blocks = np.zeros((G, k, B), np.uint8)
+    exp_cnt = np.zeros(G, np.int64)
+    for g in range(G):
+        rc, rec = ora.encode(k, m, data[g], B)
+        assert rc == 0
+        whole = np.concatenate([data[g], rec])
+        kind = g % 7
+        e = 0 if kind == 3 else int(rng.integers(1, min(k, m) + 1))
+        lost = rng.choice(k, size=e, replace=False)
+        recv = k + rng.choice(m, size=e, replace=False)
+        r = np.array(sorted(set(range(k)) - set(lost.tolist())) + recv.tolist())
+        rng.shuffle(r)
+        if kind == 5 and e >= 1:       # a recovery row listed twice
+            i0 = int(np.flatnonzero(r >= k)[0])
+            j0 = int(np.flatnonzero(r < k)[0])
+            r[j0] = r[i0]
+        elif kind == 6:                 # a row past the generator
+            r[int(rng.integers(k))] = k + m
+        rows[g] = r
+        blocks[g] = whole[np.minimum(r, k + m - 1)]  # a malformed group's bytes are never read
+        exp_cnt[g] = -1 if (kind == 5 and e >= 1) or kind == 6 else e
+    d_blocks, d_rows = _dev(blocks), _dev(rows)
+    out = torch.zeros((G, m, B), dtype=torch.uint8, device="cuda")
+    orow = torch.zeros((G, m), dtype=torch.uint8, device="cuda")
+    ocnt = torch.zeros(G, dtype=torch.int32, device="cuda")
+    sh.batch_errors()
+    assert sh.decode_batch_out(k, m, B, G, d_blocks, d_rows, out, orow, ocnt) == 0
+    assert sh.batch_errors() == int((exp_cnt < 0).sum())
+    cnt = ocnt.cpu().numpy()
+    assert np.array_equal(cnt, exp_cnt)
+    o, orr = out.cpu().numpy(), orow.cpu().numpy()
+    for g in range(G):
+        e = int(cnt[g])
+        if e <= 0:
+            continue
+        b = [x.copy() for x in blocks[g]]
+        rc, nr = ora.decode(k, m, b, rows[g].tolist(), B)
+        assert rc == 0
+        rec_pos = [i for i in range(k) if rows[g][i] >= k]
+        assert [nr[p] for p in rec_pos] == orr[g, :e].tolist(), g
+        for l, p in enumerate(rec_pos):
+            assert np.array_equal(o[g, l], b[p]), (g, l)
+            assert np.array_equal(o[g, l], data[g, nr[p]]), (g, l)
+    # in-place form: valid groups decoded, malformed ones untouched
+    d_rows2 = _dev(rows)
+    assert sh.decode_batch(k, m, B, G, d_blocks, d_rows2) == 0
+    assert sh.batch_errors() == int((exp_cnt < 0).sum())
+    nb, nr2 = d_blocks.cpu().numpy(), d_rows2.cpu().numpy()
+    for g in range(G):
+        if exp_cnt[g] < 0:
+            assert np.array_equal(nb[g], blocks[g]) and np.array_equal(nr2[g], rows[g]), g
+        else:
+            assert np.array_equal(nb[g], data[g, nr2[g].astype(np.int64)]), g
+
+
 def test_malformed_groups_reported(sh):
     """A row listed twice (outside the reference's contract) leaves the group untouched, flags it
     with count -1 and is counted by cauchy_256_batch_errors; the single-group call returns -1."""
