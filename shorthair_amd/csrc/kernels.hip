@@ -547,19 +547,119 @@ __global__ __launch_bounds__(64 * W, 8) void decode_setup(DecodeSetupArgs a, int
 }
 
 // ---------------------------------------------------------------------------------------------
-// Decode setup for the searched generators (m <= 6) in fixed-kernel mode: eight lanes per group,
-// eight groups per wave. Same outputs as decode_setup above; there a wave spends a chain of
-// dependent LDS / global round trips on one group with e <= 6, so a (28,4,256) batch of 209,263
-// groups ran ~25 rounds of resident waves (0.215 ms of a 0.743 ms decode). Here a wave carries 8
-// groups through the same chain and a row of the e x 2e Gauss-Jordan lives in one lane.
+// Multi-group decode setups (fixed-kernel mode): L lanes per group, 64 / L groups per wave. Same
+// outputs as decode_setup above; there one wave carries one group through a chain of dependent
+// LDS / global round trips, so a batch of many small groups runs many rounds of resident waves
+// ((28,4,256), 209,263 groups: 0.215 ms of a 0.743 ms decode). Here a wave carries 64 / L groups
+// through the same chain:
+//   decode_setup_small   m <= 6, L = 8: the searched tables, Gauss-Jordan with a row per lane
+//   decode_setup_cauchy  m >= 7, emax <= L = 16: the closed-form Cauchy inverse (L = 32 at e = 32
+//                        lost to the one-wave kernel: 0.073 vs 0.063 ms at (224,32,256))
 // ---------------------------------------------------------------------------------------------
-struct SmallScratch {
+// Per-group scratch: EC >= emax entries in the lists, RP >= round4(m) in the rpos image.
+template <int EC, int RP>
+struct GroupScratch {
     uint8_t rows[256];
-    uint8_t pos[256];       // pos table image (round4(k) <= 252 entries)
+    uint8_t pos[256];       // pos table image (round4(k) <= 256 entries)
     uint32_t present[8];    // bitmap of row values
-    uint8_t rpos[8];        // rpos table image (round4(m) <= 8 entries)
-    uint8_t rec[8], rrow[8], era[8];
+    uint8_t rpos[RP];       // rpos table image
+    uint8_t rec[EC], rrow[EC], era[EC];
 };
+
+__device__ __forceinline__ void group_fail(const DecodeSetupArgs &a, int g, int l) {
+    if (l == 0) {
+        a.e_out[g] = -1;
+        if (a.errors) atomicAdd(a.errors, 1);
+    }
+}
+
+// bit l of the result = predicate of lane l of the group whose first lane is gb
+template <int L>
+__device__ __forceinline__ unsigned group_ballot(bool p, int gb) {
+    return static_cast<unsigned>((__ballot(p) >> gb) & ((1ull << L) - 1ull));
+}
+
+// Before the workgroup's staging barrier: the group's row bytes (all loads in flight together),
+// present bitmap cleared.
+template <int L, class GS>
+__device__ __forceinline__ void group_load_rows(const DecodeSetupArgs &a, int g, int l, GS &S) {
+    const uint8_t *rows = a.rows + static_cast<long long>(g) * a.rows_gstride;
+    for (int j = l; j < a.k; j += L) S.rows[j] = rows[j];
+    for (int t = l; t < 8; t += L) S.present[t] = 0;
+}
+
+// After the barrier: malformed check, ordered compaction, position tables, e and the per-group
+// lists. Returns e when coefficients remain to be written, 0 when the group is done.
+template <int L, int EC, class GS>
+__device__ int group_prologue(const DecodeSetupArgs &a, int g, int l, int gb, GS &S) {
+    const int k = a.k, m = a.m;
+    // A row listed twice, or a recovery row past the generator, is outside the reference's
+    // contract (decode_setup above): the group is left untouched and reported.
+    bool bad = false;
+    for (int j = l; j < k; j += L) {
+        const int row = S.rows[j];
+        const uint32_t bit = 1u << (row & 31);
+        bad |= (atomicOr(&S.present[row >> 5], bit) & bit) != 0u || row >= k + m;
+    }
+    if (group_ballot<L>(bad, gb)) {
+        group_fail(a, g, l);
+        return 0;
+    }
+    SH_WAVE_SYNC();
+    // L entries per step: recovery blocks in array order (unique rows in [k, k+m): at most
+    // min(k, m) = emax <= EC of them), erased originals ascending (the first EC are kept).
+    int nrec = 0, nera = 0;
+    const unsigned below = (1u << l) - 1u;
+    for (int base = 0; base < k; base += L) {
+        const int j = base + l;
+        const int row = j < k ? S.rows[j] : 0;
+        const bool isrec = j < k && row >= k;
+        const bool miss = j < k && ((S.present[j >> 5] >> (j & 31)) & 1u) == 0u;
+        const unsigned mr = group_ballot<L>(isrec, gb), me = group_ballot<L>(miss, gb);
+        if (isrec) {
+            const int p = nrec + __popc(mr & below);
+            if (p < EC) {
+                S.rec[p] = static_cast<uint8_t>(j);
+                S.rrow[p] = static_cast<uint8_t>(row - k);
+            }
+        }
+        if (miss) {
+            const int p = nera + __popc(me & below);
+            if (p < EC) S.era[p] = static_cast<uint8_t>(j);
+        }
+        nrec += __popc(mr);
+        nera += __popc(me);
+    }
+    // position tables, assembled in LDS and stored as dwords
+    const int KP = (k + 3) & ~3, MP = (m + 3) & ~3;
+    for (int x = l; x < KP; x += L) S.pos[x] = 0xFF;
+    for (int y = l; y < MP; y += L) S.rpos[y] = 0xFF;
+    SH_WAVE_SYNC();
+    for (int j = l; j < k; j += L) {
+        const int row = S.rows[j];
+        if (row < k) S.pos[row] = static_cast<uint8_t>(j);
+        else S.rpos[row - k] = static_cast<uint8_t>(j);
+    }
+    SH_WAVE_SYNC();
+    uint32_t *pos = reinterpret_cast<uint32_t *>(a.pos + static_cast<long long>(g) * KP);
+    for (int t = l; t < KP / 4; t += L) pos[t] = reinterpret_cast<const uint32_t *>(S.pos)[t];
+    uint32_t *rpos = reinterpret_cast<uint32_t *>(a.rpos + static_cast<long long>(g) * MP);
+    for (int t = l; t < MP / 4; t += L) rpos[t] = reinterpret_cast<const uint32_t *>(S.rpos)[t];
+    const int e = nrec;
+    if (l == 0) a.e_out[g] = e;
+    if (e == 0) return 0;
+    if (nera < e || e > EC) {  // unreachable with unique rows and emax <= EC
+        group_fail(a, g, l);
+        return 0;
+    }
+    const int emax = a.emax;
+    for (int i = l; i < e; i += L) {
+        a.rec_idx[static_cast<long long>(g) * emax + i] = S.rec[i];
+        a.erasures[static_cast<long long>(g) * emax + i] = S.era[i];
+        a.rrow[static_cast<long long>(g) * a.ldR + i] = S.rrow[i];
+    }
+    return e;
+}
 
 // One Gauss-Jordan row of up to 12 bytes in three registers (byte c at bits 8 (c & 3) of word
 // c >> 2); every index goes through selects, so no array is ever placed in scratch.
@@ -593,111 +693,40 @@ struct Row12 {
 
 template <int W>
 __global__ __launch_bounds__(64 * W, 8) void decode_setup_small(DecodeSetupArgs a, int groups) {
+    constexpr int L = 8;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int sub = lane >> 3, l = lane & 7, gb = 8 * sub;  // gb: first lane of this group
-    const int g = (blockIdx.x * W + wave) * 8 + sub;
+    const int sub = lane / L, l = lane % L, gb = L * sub;  // gb: first lane of this group
+    const int g = (blockIdx.x * W + wave) * (64 / L) + sub;
     const int k = a.k, m = a.m;
     __shared__ uint8_t s_exp[512];
     __shared__ uint8_t s_log[256];
     __shared__ uint8_t s_gen[5 * 256];
-    __shared__ SmallScratch sw[8 * W];
-    SmallScratch &S = sw[8 * wave + sub];
+    __shared__ GroupScratch<8, 8> sw[(64 / L) * W];
+    GroupScratch<8, 8> &S = sw[(64 / L) * wave + sub];
     const bool live = g < groups;
-    if (live) {  // the group's row bytes (all loads in flight together), present bitmap cleared
-        const uint8_t *rows = a.rows + static_cast<long long>(g) * a.rows_gstride;
-        for (int j = l; j < k; j += 8) S.rows[j] = rows[j];
-        S.present[l] = 0;
-    }
+    if (live) group_load_rows<L>(a, g, l, S);
     for (int i = threadIdx.x; i < 512; i += 64 * W) s_exp[i] = a.gf_exp[i];
     for (int i = threadIdx.x; i < 256; i += 64 * W) s_log[i] = static_cast<uint8_t>(a.gf_log[i]);
     for (int i = threadIdx.x; i < (m - 1) * k; i += 64 * W) s_gen[i] = a.gen[i];
     __syncthreads();  // the only workgroup barrier: groups below may finish independently
     if (!live) return;
-    // group-local ballot: bit l of the result = predicate of lane l of this group
-    auto gballot = [&](bool p) { return static_cast<unsigned>((__ballot(p) >> gb) & 0xFFull); };
-    auto fail = [&]() {
-        if (l == 0) {
-            a.e_out[g] = -1;
-            if (a.errors) atomicAdd(a.errors, 1);
-        }
-    };
-    // A row listed twice, or a recovery row past the generator, is outside the reference's
-    // contract (decode_setup above): the group is left untouched and reported.
-    bool bad = false;
-    for (int j = l; j < k; j += 8) {
-        const int row = S.rows[j];
-        const uint32_t bit = 1u << (row & 31);
-        bad |= (atomicOr(&S.present[row >> 5], bit) & bit) != 0u || row >= k + m;
-    }
-    if (gballot(bad)) {
-        fail();
-        return;
-    }
-    SH_WAVE_SYNC();
-    // Ordered compaction, eight entries per step: recovery blocks in array order (unique rows in
-    // [k, k+m): at most m of them), erased originals ascending (the first 8 are kept; e <= m).
-    int nrec = 0, nera = 0;
-    for (int base = 0; base < k; base += 8) {
-        const int j = base + l;
-        const int row = j < k ? S.rows[j] : 0;
-        const bool isrec = j < k && row >= k;
-        const bool miss = j < k && ((S.present[j >> 5] >> (j & 31)) & 1u) == 0u;
-        const unsigned mr = gballot(isrec), me = gballot(miss);
-        const unsigned below = (1u << l) - 1u;
-        if (isrec) {
-            const int p = nrec + __popc(mr & below);
-            S.rec[p] = static_cast<uint8_t>(j);
-            S.rrow[p] = static_cast<uint8_t>(row - k);
-        }
-        if (miss) {
-            const int p = nera + __popc(me & below);
-            if (p < 8) S.era[p] = static_cast<uint8_t>(j);
-        }
-        nrec += __popc(mr);
-        nera += __popc(me);
-    }
-    // position tables, assembled in LDS and stored as dwords
-    const int KP = (k + 3) & ~3, MP = (m + 3) & ~3;
-    for (int x = l; x < KP; x += 8) S.pos[x] = 0xFF;
-    S.rpos[l] = 0xFF;
-    SH_WAVE_SYNC();
-    for (int j = l; j < k; j += 8) {
-        const int row = S.rows[j];
-        if (row < k) S.pos[row] = static_cast<uint8_t>(j);
-        else S.rpos[row - k] = static_cast<uint8_t>(j);
-    }
-    SH_WAVE_SYNC();
-    {
-        uint32_t *pos = reinterpret_cast<uint32_t *>(a.pos + static_cast<long long>(g) * KP);
-        for (int t = l; t < KP / 4; t += 8) pos[t] = reinterpret_cast<const uint32_t *>(S.pos)[t];
-        uint32_t *rpos = reinterpret_cast<uint32_t *>(a.rpos + static_cast<long long>(g) * MP);
-        if (l < MP / 4) rpos[l] = reinterpret_cast<const uint32_t *>(S.rpos)[l];
-    }
-    const int e = nrec;
-    if (l == 0) a.e_out[g] = e;
+    const int e = group_prologue<L, 8>(a, g, l, gb, S);
     if (e == 0) return;
-    if (nera < e) {  // unreachable with unique rows; kept as in decode_setup
-        fail();
-        return;
-    }
     const int emax = a.emax;
-    if (l < e) {
-        a.rec_idx[static_cast<long long>(g) * emax + l] = S.rec[l];
-        a.erasures[static_cast<long long>(g) * emax + l] = S.era[l];
-        a.rrow[static_cast<long long>(g) * a.ldR + l] = S.rrow[l];
-    }
     uint8_t *Bc = a.targets ? nullptr : a.coefB + static_cast<long long>(g) * a.coefB_gstride;
     uint64_t *Tg = a.targets ? a.targets + static_cast<long long>(g) * emax * a.ldB : nullptr;
     const uint64_t tnull = a.snip_base + static_cast<uint64_t>(SNIP_NULL) * SNIP_STRIDE;
     if (Tg) {  // null snippet for the unused outputs j in [e, ldB)
         const int pad = a.ldB - e;
-        for (int t = l; t < e * pad; t += 8) {
+        for (int t = l; t < e * pad; t += L) {
             const int i = t / pad, j = e + (t - i * pad);
             Tg[(static_cast<long long>(j >> 3) * emax + i) * 8 + (j & 7)] = tnull;
         }
     } else {
-        for (int t = l; t < emax * a.ldB; t += 8) Bc[t] = 0;
+        for (int t = l; t < emax * a.ldB; t += L) Bc[t] = 0;
     }
+    auto gballot = [&](bool p) { return group_ballot<L>(p, gb); };
+    auto fail = [&]() { group_fail(a, g, l); };
 
     // Gauss-Jordan on [S | I], S[i][j] = C[r_i][E_j]: lane l < e holds row l (2e <= 12 bytes).
     Row12 u;
@@ -745,6 +774,109 @@ __global__ __launch_bounds__(64 * W, 8) void decode_setup_small(DecodeSetupArgs 
                 Tg[static_cast<long long>(i) * 8 + l] = v ? a.snip_base + static_cast<uint64_t>(v) * SNIP_STRIDE : tnull;
             else
                 Bc[static_cast<long long>(i) * a.ldB + l] = static_cast<uint8_t>(v);
+        }
+    }
+}
+
+// Closed-form S^-1 (m >= 7, decode_setup above) for emax <= L: x_j, y_i, the la / lb sums and
+// the coefficient walk spread over the group's L lanes instead of a wave.
+template <int EC>
+struct CauchyLists {
+    uint8_t x[EC], y[EC], la[EC], lb[EC];
+};
+
+template <int W, int L>
+__global__ __launch_bounds__(64 * W, 8) void decode_setup_cauchy(DecodeSetupArgs a, int groups) {
+    static_assert(L % 8 == 0 && L <= 32, "group lanes: a multiple of 8, at most 32");
+    constexpr int GPW = 64 / L;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int sub = lane / L, l = lane % L, gb = L * sub;
+    const int g = (blockIdx.x * W + wave) * GPW + sub;
+    const int k = a.k, m = a.m;
+    __shared__ uint8_t s_exp[1024];  // exp(i mod 255): exponent sums up to 763 unreduced
+    __shared__ uint8_t s_log[256];
+    __shared__ uint8_t s_xp[256], s_yp[256];
+    __shared__ GroupScratch<L, 256> sw[GPW * W];
+    __shared__ CauchyLists<L> cw[GPW * W];
+    GroupScratch<L, 256> &S = sw[GPW * wave + sub];
+    CauchyLists<L> &X = cw[GPW * wave + sub];
+    const bool live = g < groups;
+    if (live) group_load_rows<L>(a, g, l, S);
+    static_assert(64 * W * 4 >= 1024, "four exp entries per thread");
+    {
+        uint8_t ev[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ev[u] = a.gf_exp[(4 * threadIdx.x + u) % 255];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s_exp[4 * threadIdx.x + u] = ev[u];
+    }
+    for (int i = threadIdx.x; i < 256; i += 64 * W) s_log[i] = static_cast<uint8_t>(a.gf_log[i]);
+    for (int i = threadIdx.x; i < k; i += 64 * W) s_xp[i] = a.xp[i];
+    for (int i = threadIdx.x; i < m; i += 64 * W) s_yp[i] = a.yp[i];
+    __syncthreads();  // the only workgroup barrier: groups below may finish independently
+    if (!live) return;
+    const int e = group_prologue<L, L>(a, g, l, gb, S);
+    if (e == 0) return;
+    for (int t = l; t < e; t += L) {
+        X.x[t] = s_xp[S.era[t]];
+        X.y[t] = s_yp[S.rrow[t]];
+    }
+    SH_WAVE_SYNC();
+    // log a_j - log x_j (items w < e) and log b_i (items e <= w < 2e), as in decode_setup
+    for (int w = l; w < 2 * e; w += L) {
+        const bool isa = w < e;
+        const int t = isa ? w : w - e;
+        const uint8_t *other = isa ? X.y : X.x;
+        const uint8_t *own = isa ? X.x : X.y;
+        const int me = own[t];
+        int acc = isa ? 255 * 130 - s_log[me] : 255 * 130;  // offset keeps the sum positive
+#pragma unroll 4
+        for (int q = 0; q < e; ++q) {
+            acc += s_log[me ^ other[q]];
+            acc -= q != t ? s_log[me ^ own[q]] : 0;
+        }
+        (isa ? X.la : X.lb)[t] = static_cast<uint8_t>(acc % 255);
+    }
+    SH_WAVE_SYNC();
+    auto coef = [&](int j, int i) -> uint32_t {
+        return s_exp[X.la[j] + X.lb[i] + 255 - s_log[X.x[j] ^ X.y[i]]];
+    };
+    const int emax = a.emax, ldB = a.ldB;
+    if (a.targets) {
+        // addresses [j/8][i][j%8] for i < e, in memory order: lane l keeps j%8 = l%8 (L is a
+        // multiple of 8) and steps i by L/8, carrying into the next block of 8 outputs
+        uint64_t *Tg = a.targets + static_cast<long long>(g) * emax * ldB;
+        const uint64_t tnull = a.snip_base + static_cast<uint64_t>(SNIP_NULL) * SNIP_STRIDE;
+        const int jj = l & 7, nb = ldB >> 3;
+        int i = l >> 3, jb = 0;
+        while (i >= e) {
+            i -= e;
+            ++jb;
+        }
+        while (jb < nb) {
+            const int j = jb * 8 + jj;
+            const uint32_t c = j < e ? coef(j, i) : 0u;
+            Tg[(static_cast<long long>(jb) * emax + i) * 8 + jj] =
+                c ? a.snip_base + static_cast<uint64_t>(c) * SNIP_STRIDE : tnull;
+            i += L / 8;
+            while (i >= e) {
+                i -= e;
+                ++jb;
+            }
+        }
+    } else {
+        // bytes [i][j], i < emax, j < ldB, zero outside (i < e, j < e)
+        uint8_t *Bc = a.coefB + static_cast<long long>(g) * a.coefB_gstride;
+        const int iinc = L / ldB, jinc = L - iinc * ldB, n = emax * ldB;
+        int i = l / ldB, j = l - i * ldB;
+        for (int t = l; t < n; t += L) {
+            Bc[t] = static_cast<uint8_t>(i < e && j < e ? coef(j, i) : 0u);
+            j += jinc;
+            i += iinc;
+            if (j >= ldB) {
+                j -= ldB;
+                ++i;
+            }
         }
     }
 }
@@ -904,12 +1036,25 @@ hipError_t launch_copy_first(const uint8_t *in, long long in_gstride, uint8_t *o
 
 hipError_t launch_decode_setup(const DecodeSetupArgs &a, int groups, hipStream_t stream) {
     constexpr int W = 4;
-    // measurement builds: SH_SETUP_WAVE=1 runs the one-wave-per-group kernel for every shape
+    // The multi-group setups pay a longer per-group chain for fewer rounds of waves: they win once
+    // the one-wave kernel needs more than one round (256 CUs x 32 resident waves = 8192 groups);
+    // below that the one-wave kernel is as fast or faster (profiles/r06/ab_runs.txt, block 8).
+    // Measurement builds: SH_SETUP_WAVE=1 runs the one-wave kernel for every shape,
+    // SH_SETUP_MIN_SMALL / SH_SETUP_MIN_CAUCHY move the thresholds.
     static const bool wave_only = measure_int(SH_MEASURE_ENV("SH_SETUP_WAVE"), 0) != 0;
-    if (a.coefA == nullptr && a.m <= 6 && a.k <= 250 && !wave_only) {
-        hipLaunchKernelGGL(decode_setup_small<W>, dim3((groups + 8 * W - 1) / (8 * W)), dim3(64 * W), 0, stream,
-                           a, groups);
-        return hipGetLastError();
+    static const int min_small = measure_int(SH_MEASURE_ENV("SH_SETUP_MIN_SMALL"), 8192);
+    static const int min_cauchy = measure_int(SH_MEASURE_ENV("SH_SETUP_MIN_CAUCHY"), 8192);
+    if (a.coefA == nullptr && !wave_only) {
+        if (a.m <= 6 && groups >= min_small) {
+            hipLaunchKernelGGL(decode_setup_small<W>, dim3((groups + 8 * W - 1) / (8 * W)), dim3(64 * W), 0,
+                               stream, a, groups);
+            return hipGetLastError();
+        }
+        if (a.m >= 7 && a.emax <= 16 && groups >= min_cauchy) {
+            hipLaunchKernelGGL((decode_setup_cauchy<W, 16>), dim3((groups + 4 * W - 1) / (4 * W)), dim3(64 * W), 0,
+                               stream, a, groups);
+            return hipGetLastError();
+        }
     }
     hipLaunchKernelGGL(decode_setup<W>, dim3((groups + W - 1) / W), dim3(64 * W), 0, stream, a, groups);
     return hipGetLastError();

@@ -443,11 +443,11 @@ def test_searched_table_setup_mixed_groups(sh, k, m, B):
             i0 = int(np.flatnonzero(r >= k)[0])
             j0 = int(np.flatnonzero(r < k)[0])
             r[j0] = r[i0]
-        elif kind == 6:                 # a row past the generator
+        elif kind == 6 and k + m < 256:  # a row past the generator (a byte value)
             r[int(rng.integers(k))] = k + m
         rows[g] = r
         blocks[g] = whole[np.minimum(r, k + m - 1)]  # a malformed group's bytes are never read
-        exp_cnt[g] = -1 if (kind == 5 and e >= 1) or kind == 6 else e
+        exp_cnt[g] = -1 if (kind == 5 and e >= 1) or (kind == 6 and k + m < 256) else e
     d_blocks, d_rows = _dev(blocks), _dev(rows)
     out = torch.zeros((G, m, B), dtype=torch.uint8, device="cuda")
     orow = torch.zeros((G, m), dtype=torch.uint8, device="cuda")
@@ -480,6 +480,78 @@ def test_searched_table_setup_mixed_groups(sh, k, m, B):
             assert np.array_equal(nb[g], blocks[g]) and np.array_equal(nr2[g], rows[g]), g
         else:
             assert np.array_equal(nb[g], data[g, nr2[g].astype(np.int64)]), g
+
+
+@pytest.mark.parametrize("k,m,B", [(50, 10, 1000), (8, 20, 1400), (64, 16, 264), (12, 7, 1400),
+                                   (28, 4, 256), (20, 6, 1400), (250, 6, 1400), (40, 2, 512)])
+def test_multi_group_setup_mixed_groups_many(sh, k, m, B):
+    """More than 8192 groups, where the multi-group setups run (m >= 7 with emax <= 16:
+    decode_setup_cauchy, 16 lanes per group; m <= 6: decode_setup_small, 8 lanes per group):
+    random e and array order, e = 0, duplicated and out-of-range rows side by side. Counts and
+    error count exact, every valid group's recovered blocks equal the encoded originals, row
+    contract and bytes of sampled groups against the oracle's decode."""
+    import torch
+    G = 8300
+    rng = np.random.default_rng(k * 131 + m)
+    data = torch.empty((G, k, B), dtype=torch.uint8, device="cuda")
+    rec = torch.empty((G, m, B), dtype=torch.uint8, device="cuda")
+    assert sh.fill_synthetic(data, k, B, G, 0, 0x3C) == 0
+    assert sh.encode_batch(k, m, B, G, data, rec) == 0
+    emax = min(k, m)
+    rows = np.zeros((G, k), np.int64)
+    exp_cnt = np.zeros(G, np.int64)
+    for g in range(G):
+        kind = g % 7
+        e = 0 if kind == 3 else int(rng.integers(1, emax + 1))
+        lost = rng.choice(k, size=e, replace=False)
+        recv = k + rng.choice(m, size=e, replace=False)
+        keep = np.setdiff1d(np.arange(k), lost)
+        r = np.concatenate([keep, recv])
+        rng.shuffle(r)
+        if kind == 5 and e >= 1:      # a recovery row listed twice (over an original if any)
+            i0 = int(np.flatnonzero(r >= k)[0])
+            others = np.flatnonzero(np.arange(k) != i0)
+            r[int(others[0])] = r[i0]
+        elif kind == 6 and k + m < 256:  # a row past the generator (a byte value)
+            r[int(rng.integers(k))] = k + m
+        rows[g] = r
+        exp_cnt[g] = -1 if (kind == 5 and e >= 1) or (kind == 6 and k + m < 256) else e
+    whole = torch.cat([data, rec], dim=1)
+    d_rows = torch.from_numpy(rows.astype(np.uint8)).cuda()
+    idx = torch.from_numpy(np.minimum(rows, k + m - 1)).cuda()
+    blocks = whole[torch.arange(G, device="cuda")[:, None], idx].contiguous()
+    del whole
+    out = torch.zeros((G, emax, B), dtype=torch.uint8, device="cuda")
+    orow = torch.zeros((G, emax), dtype=torch.uint8, device="cuda")
+    ocnt = torch.zeros(G, dtype=torch.int32, device="cuda")
+    sh.batch_errors()
+    assert sh.decode_batch_out(k, m, B, G, blocks, d_rows, out, orow, ocnt) == 0
+    assert sh.batch_errors() == int((exp_cnt < 0).sum())
+    cnt = ocnt.cpu().numpy()
+    assert np.array_equal(cnt, exp_cnt)
+    # recovered blocks = the originals named by out_rows (valid groups, first e entries)
+    valid = torch.from_numpy(cnt).cuda()
+    truth = data[torch.arange(G, device="cuda")[:, None], orow.long()]
+    mask = torch.arange(emax, device="cuda")[None, :] < valid[:, None]
+    assert torch.equal(out[mask], truth[mask])
+    # out_rows: the erased originals ascending (reference row contract)
+    orr = orow.cpu().numpy()
+    for g in range(0, G, 97):
+        e = int(cnt[g])
+        if e > 0:
+            missing = np.setdiff1d(np.arange(k), rows[g][rows[g] < k])[:e]
+            assert orr[g, :e].tolist() == missing.tolist(), g
+    ora = po.oracle()
+    for g in (1, G // 2 + 1, G - 2):
+        if exp_cnt[g] <= 0:
+            continue
+        b = [x.copy() for x in blocks[g].cpu().numpy()]
+        rc, nr = ora.decode(k, m, b, rows[g].tolist(), B)
+        assert rc == 0
+        rec_pos = [i for i in range(k) if rows[g][i] >= k]
+        o = out[g].cpu().numpy()
+        for l, p in enumerate(rec_pos):
+            assert nr[p] == orr[g, l] and np.array_equal(o[l], b[p]), (g, l)
 
 
 def test_malformed_groups_reported(sh):
