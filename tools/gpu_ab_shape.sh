@@ -1,12 +1,20 @@
 #!/bin/bash
-# Per-op device times of library variants at one shape (measurement only):
-#   tools/gpu_ab_shape.sh K M B GROUPS VARIANT [VARIANT ...]     (main = shorthair_amd/libcauchy256.so)
+# Same-box A/B of library variants at one shape and several batch sizes (measurement only):
+#   tools/gpu_ab_shape.sh "NAME[,NAME...]" K M B E G[,G...]
 set -u
-K=$1 M=$2 B=$3 G=$4; shift 4
-E=$(( K < M ? K : M ))
-for v in "$@"; do
-  L=$PWD/shorthair_amd/libcauchy256_$v.so; [ "$v" = main ] && L=$PWD/shorthair_amd/libcauchy256.so
-  printf "%-8s (%d,%d,%d) " "$v" "$K" "$M" "$B"
-  SH_LIB_PATH=$L timeout -k 10 120 python tools/run_ops.py --op both --iters 10 --k "$K" --m "$M" --block "$B" \
-      --groups "$G" --erasures "$E" 2>&1 | grep -v amdgpu.ids | tail -1 || exit 1
+VARS=$1 K=$2 M=$3 B=$4 E=$5 GS=$6
+lib() { if [ "$1" = main ]; then echo "$PWD/shorthair_amd/libcauchy256.so"; else echo "$PWD/shorthair_amd/libcauchy256_$1.so"; fi; }
+for round in 1 2; do
+  for G in $(echo "$GS" | tr , ' '); do
+    for v in $(echo "$VARS" | tr , ' '); do
+      printf "%-8s G=%-6s " "$v" "$G"
+      SH_LIB_PATH=$(lib "$v") timeout -k 10 120 python tools/run_ops.py --op both --iters 20 --k $K --m $M --block $B --groups $G --erasures $E 2>&1 | grep -v amdgpu.ids | tail -1
+      [ "${PIPESTATUS[0]}" = 0 ] || exit 1
+    done
+  done
+done
+for v in $(echo "$VARS" | tr , ' '); do
+  printf "%-8s " "$v"
+  SH_LIB_PATH=$(lib "$v") timeout -k 10 120 python tools/run_ops.py --op both --iters 1 --digest --k $K --m $M --block $B --groups 4096 --erasures $E 2>&1 | grep digest
+  [ "${PIPESTATUS[0]}" = 0 ] || exit 1
 done
