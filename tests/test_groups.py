@@ -191,3 +191,46 @@ def test_groups_multi_chunk_headline_shape(ora):
         assert pid in lost_sets[g] and groups[g][1][pid] == p
     sample = [d for d in delivered if d[0] == 123]
     assert [(pid, p) for _, pid, p in sample] == opk.rx_group(ora, *rx[123])
+
+
+@pytest.mark.gpu
+def test_groups_concurrent_calls(ora):
+    """Two threads frame and recover packet groups at once: a framing pass that finds
+    the host worker pool busy runs on its own thread, so both calls progress; every result exact."""
+    import threading
+    from shorthair_amd import groups as sg
+    errors = []
+
+    def worker(seed):
+        try:
+            groups = _mixed_groups(seed, 33)
+            for _ in range(3):
+                recs = sg.encode_groups(groups)
+                for (m, pk), rec in zip(groups, recs):
+                    assert rec == opk.tx_group(ora, m, pk)
+                rng = random.Random(seed)
+                rx, lost_sets = [], []
+                for (m, pk), rec in zip(groups, recs):
+                    k = len(pk)
+                    if k == 1:
+                        lost, orig, got = {0}, [], rec[:1]
+                    else:
+                        e = rng.randint(1, min(k, len(rec)))
+                        lost, orig, got = _lose(rng, k, pk, rec, e, e)
+                    rx.append((orig, got))
+                    lost_sets.append(lost)
+                n, delivered = sg.recover_groups(rx)
+                assert n == len(groups)
+                for g, pid, p in delivered:
+                    assert pid in lost_sets[g] and groups[g][1][pid] == p
+                assert len(delivered) == sum(len(s) for s in lost_sets)
+        except Exception as ex:  # reported on the main thread
+            errors.append((seed, repr(ex)))
+
+    threads = [threading.Thread(target=worker, args=(s,)) for s in (31, 32)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=120)
+    assert not any(th.is_alive() for th in threads)
+    assert not errors, errors
