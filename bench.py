@@ -583,6 +583,10 @@ def main():
             # a bounded collective timeout: a stuck side leg raises (and is reported) instead of
             # holding the job past the driver's limit
             import datetime
+            # on a timeout the watchdog aborts the communicators but leaves the process alive
+            # (torch's default kills it), so a stuck root-resident leg surfaces as an exception
+            # in that leg and the main line, measured before it, still prints
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev),
                                     timeout=datetime.timedelta(seconds=args.pg_timeout))
         else:
