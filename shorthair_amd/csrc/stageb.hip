@@ -847,6 +847,134 @@ __global__ __launch_bounds__(64) void stageb_small(StageBSmallArgs a) {
     }
 }
 
+// Two word columns per lane (stageb_small2): the two columns of a lane belong to one group, so
+// both take the same table entry for a coefficient and one ds_read_b64 fetches the pair — the
+// LDS array serves 8-byte reads at twice the 4-byte rate (MI355X_MICROARCH.md §LDS: ~150 vs
+// ~75 TB/s chip-wide), and the lookups are most of stageb_small's LDS time. Table layout
+// [half][entry][lane & 31] of uint2 (half = lane >> 5, 8 KB each), so an address is still one
+// v_perm_b32: entry + 32 * half in byte 1 (pre-added in the half's copy of the entry table) and
+// (lane & 31) * 8 in byte 0. Per launch at (224,32,256) (PMC, ab_runs block 10): LDS instructions
+// 6.4e7 -> 3.2e7, VALU 1.14e8 -> 7.8e7; with 24 KB of LDS and 212 VGPRs a CU holds 6 of these
+// waves (11-13 of stageb_small's), so the stage gains 7 %, not the halved lookup time.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+__global__ __launch_bounds__(64) void stageb_small2(StageBSmallArgs a) {
+    __shared__ __attribute__((aligned(16))) u32x2 tab[2 * 32 * 32];        // 16 KB window tables
+    __shared__ __attribute__((aligned(16))) uint32_t rbt[2 * 256 * 4];     // entry bytes per half
+    extern __shared__ uint8_t rrs[];
+    const Geometry geo = a.geo;
+    const int lane = threadIdx.x;
+    const int lpg = geo.nq / 2;  // lanes per group
+    const int gpw = 64 / lpg;
+    const int gs = lane / lpg, ql = lane - gs * lpg;
+    int gb = blockIdx.x, chunk = blockIdx.y;
+    if (a.xcd_map) {  // as stageb_small: the chunks of one group block on one XCD, back to back
+        const int nch = (a.emax + 7) / 8;
+        const int i = static_cast<int>(blockIdx.x) >> 3;
+        chunk = i % nch;
+        gb = (i / nch) * 8 + (static_cast<int>(blockIdx.x) & 7);
+        if (gb * gpw >= a.groups) return;
+    }
+    const int g0 = gb * gpw;
+    const bool valid = gs < gpw && g0 + gs < a.groups;
+    const int g = valid ? g0 + gs : g0;
+    const int j0 = chunk * 8;
+    for (int t = lane; t < 2 * 256; t += 64) {
+        const int h = t >> 8, c = t & 255;
+        uint32_t w[4] = {0, 0, 0, 0};
+        uint32_t v = static_cast<uint32_t>(c);
+        for (int b = 0; b < 8; ++b) {
+            const uint32_t lo = (v & 15u) + 32u * h, hi = 16u + (v >> 4) + 32u * h;
+            w[b >> 1] |= (lo | (hi << 8)) << (16 * (b & 1));
+            v = (v << 1) ^ ((v & 0x80u) ? 0x187u : 0u);  // c * 2^b in GF(256)/0x187
+        }
+        for (int u = 0; u < 4; ++u) rbt[t * 4 + u] = w[u];
+    }
+    const int half = lane >> 5;
+    const int lbase = half * 32 * 32 + (lane & 31);  // tab index of entry 0 for this lane
+    tab[lbase] = u32x2{0u, 0u};             // T0[0]
+    tab[lbase + 16 * 32] = u32x2{0u, 0u};   // T1[0]
+    for (int t = lane; t < gpw * a.emax; t += 64) {
+        const int sl = t / a.emax, i = t - sl * a.emax;
+        const int gg = g0 + sl;
+        rrs[sl * a.emax + i] = (gg < a.groups && i < a.e[gg]) ? a.rrow[static_cast<long long>(gg) * a.ldR + i] : 0;
+    }
+    __syncthreads();
+    const int el = valid ? max(a.e[g], 0) : 0;
+    int emx = el;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) emx = max(emx, __shfl_xor(emx, o));
+    emx = __builtin_amdgcn_readfirstlane(emx);
+    if (emx <= j0) return;
+
+    // the lane's two words are adjacent (colx_off shifts the last four columns together)
+    const uint32_t coff = colx_off(2 * ql, geo.nq, geo.sub);
+    const uint8_t *res = a.in + static_cast<long long>(g) * a.in_gstride + coff;
+    const uint8_t *cp = a.coefT + static_cast<long long>(g) * a.coefT_gstride + j0;
+    const uint32_t lane8 = static_cast<uint32_t>(lane & 31) * 8u;
+    const uint32_t *rbh = rbt + half * 256 * 4;
+    auto load = [&](int i, u32x2 (&d)[8], uint64_t &cc) {
+        const int r = valid ? rrs[gs * a.emax + min(i, max(el - 1, 0))] : 0;
+        const uint8_t *p = res + static_cast<long long>(r) * geo.B;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) __builtin_memcpy(&d[s], p + s * geo.sub, 8);
+        cc = 0;
+        if (i < el) __builtin_memcpy(&cc, cp + static_cast<long long>(i) * a.ldT, 8);
+    };
+    auto lk = [&](uint32_t addr) {
+        return *reinterpret_cast<const u32x2 *>(reinterpret_cast<const uint8_t *>(tab) + addr);
+    };
+
+    u32x2 acc[8][8];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[jj][b] = u32x2{0u, 0u};
+    u32x2 d[8];
+    uint64_t cc, ccn = 0;
+    load(0, d, cc);
+    for (int i = 0; i < emx; ++i) {
+        const u32x2 e3 = d[0] ^ d[1], e5 = d[0] ^ d[2], e6 = d[1] ^ d[2], e9 = d[0] ^ d[3];
+        const u32x2 e10 = d[1] ^ d[3], e12 = d[2] ^ d[3], e7 = e3 ^ d[2];
+        const u32x2 f3 = d[4] ^ d[5], f5 = d[4] ^ d[6], f6 = d[5] ^ d[6], f9 = d[4] ^ d[7];
+        const u32x2 f10 = d[5] ^ d[7], f12 = d[6] ^ d[7], f7 = f3 ^ d[6];
+        const u32x2 tv[32] = {{0u, 0u}, d[0], d[1], e3, d[2], e5, e6, e7, d[3], e9, e10, e3 ^ d[3], e12, e5 ^ d[3], e6 ^ d[3], e7 ^ d[3],
+                              {0u, 0u}, d[4], d[5], f3, d[6], f5, f6, f7, d[7], f9, f10, f3 ^ d[7], f12, f5 ^ d[7], f6 ^ d[7], f7 ^ d[7]};
+#pragma unroll
+        for (int t = 1; t < 32; ++t)
+            if (t != 16) tab[lbase + t * 32] = tv[t];
+        // the row's words are in LDS now: the next row loads into the same registers
+        if (i + 1 < emx) load(i + 1, d, ccn);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+            const uint32_t c = static_cast<uint32_t>(cc >> (8 * jj)) & 0xFFu;
+            const u32x4 rb = *reinterpret_cast<const u32x4 *>(&rbh[c * 4]);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const uint32_t w = rb[b >> 1];
+                const uint32_t k = 2u * (b & 1);  // byte k: T0 entry, byte k + 1: T1 entry
+                const uint32_t a0 = __builtin_amdgcn_perm(w, lane8, 0x0C0C0000u | ((4u + k) << 8));
+                const uint32_t a1 = __builtin_amdgcn_perm(w, lane8, 0x0C0C0000u | ((5u + k) << 8));
+                const u32x2 x0 = lk(a0), x1 = lk(a1);
+                acc[jj][b].x = __builtin_amdgcn_bitop3_b32(acc[jj][b].x, x0.x, x1.x, 0x96);
+                acc[jj][b].y = __builtin_amdgcn_bitop3_b32(acc[jj][b].y, x0.y, x1.y, 0x96);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        cc = ccn;
+    }
+    if (!valid) return;
+    uint8_t *out = a.out + static_cast<long long>(g) * a.out_gstride + coff;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+        if (j0 + jj >= el) break;
+        uint8_t *row = out + static_cast<long long>(j0 + jj) * geo.B;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) __builtin_memcpy(row + b * geo.sub, &acc[jj][b], 8);
+    }
+}
+
 hipError_t launch_stageb_small(const StageBSmallArgs &a, hipStream_t stream) {
     if (a.groups <= 0 || a.emax <= 0) return hipSuccess;
     if (!stageb_small_ok(a.geo, a.emax)) return hipErrorNotSupported;
@@ -855,6 +983,18 @@ hipError_t launch_stageb_small(const StageBSmallArgs &a, hipStream_t stream) {
     static const bool xcd = sh::measure_int(SH_MEASURE_ENV("SH_SMALL_XCD"), 1) != 0;  // measurement
     StageBSmallArgs m = a;
     m.xcd_map = xcd && nch > 1 ? 1 : 0;
+    // Two word columns per lane (stageb_small2, ab_runs block 10: (224,32,256) 0.410 -> 0.380 ms,
+    // (112,16,256) -2 %, (28,4,256) equal); measurement builds: SH_SMALL2=0 runs stageb_small.
+    static const bool two = sh::measure_int(SH_MEASURE_ENV("SH_SMALL2"), 1) != 0;
+    if (two) {
+        const int gpw2 = 64 / (a.geo.nq / 2);
+        const int ngb2 = (a.groups + gpw2 - 1) / gpw2;
+        const dim3 grid2 = m.xcd_map ? dim3(static_cast<unsigned>(8 * nch * ((ngb2 + 7) / 8)), 1, 1)
+                                     : dim3(static_cast<unsigned>(ngb2), static_cast<unsigned>(nch), 1);
+        const size_t rrs2 = (static_cast<size_t>(gpw2) * a.emax + 15) & ~static_cast<size_t>(15);
+        hipLaunchKernelGGL(stageb_small2, grid2, dim3(64), rrs2, stream, m);
+        return hipGetLastError();
+    }
     const dim3 grid = m.xcd_map ? dim3(static_cast<unsigned>(8 * nch * ((ngb + 7) / 8)), 1, 1)
                                 : dim3(static_cast<unsigned>(ngb), static_cast<unsigned>(nch), 1);
     const size_t rrs_bytes = (static_cast<size_t>(gpw) * a.emax + 15) & ~static_cast<size_t>(15);

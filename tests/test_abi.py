@@ -72,7 +72,7 @@ def test_field_table_pointers_exported():
 MEASUREMENT_SWITCHES = ("SH_HSACO_DIR", "SH_DEC_CHUNKS", "SH_STAGEB_OLD", "SH_FORCE_TILE", "SH_NO_TILE",
                         "SH_NO_COL", "SH_COL_ENC", "SH_SB_SLICE", "SH_SLICE_MAX", "SH_SLICE_STEPS",
                         "SH_SMALL_XCD", "SH_V2_NW", "SH_V2_NO_TAIL", "SH_V2_MIN", "SH_V2_MAX",
-                        "SH_PKT_CHUNK_MB", "SH_HOST_THREADS", "SH_SETUP_WAVE", "SH_SETUP_MIN_SMALL", "SH_SETUP_MIN_CAUCHY")
+                        "SH_PKT_CHUNK_MB", "SH_HOST_THREADS", "SH_SETUP_WAVE", "SH_SETUP_MIN_SMALL", "SH_SETUP_MIN_CAUCHY", "SH_SMALL2")
 
 
 def test_product_library_has_no_measurement_hooks():
