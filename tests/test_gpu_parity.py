@@ -483,8 +483,8 @@ def test_searched_table_setup_mixed_groups(sh, k, m, B):
 
 
 @pytest.mark.parametrize("k,m,B", [(50, 10, 1000), (8, 20, 1400), (64, 16, 264), (12, 7, 1400),
-                                   (40, 12, 256), (28, 4, 256), (20, 6, 1400), (250, 6, 1400),
-                                   (40, 2, 512)])
+                                   (40, 12, 256), (241, 15, 256), (28, 4, 256), (20, 6, 1400),
+                                   (250, 6, 1400), (40, 2, 512)])
 def test_multi_group_setup_mixed_groups_many(sh, k, m, B):
     """More than 8192 groups, where the multi-group setups run (m >= 7 with emax <= 16:
     decode_setup_cauchy, 16 lanes per group; m <= 6: decode_setup_small, 8 lanes per group):
