@@ -571,6 +571,8 @@ struct DecodeWS {
     bool small;       // ... and stage B by stageb_small (nq <= 16 word columns: byte coefficients)
     bool v2;          // ... or by stageb_v2 (byte coefficients, one workgroup per group chunk)
     int emax, ldA, ldB, nres;  // nres: residual rows per group (m when fixed, else emax)
+    int kp;           // position-table stride: round4 of the stage-A kernel's K (a compiled K > k
+                      // codes k, sh::fixed_kernel_k; the entries past k stay 0xFF)
     int *e;
     uint8_t *rec_idx, *erasures, *coefA, *coefB, *residual, *recovered, *pos, *rpos, *rrow;
     uint64_t *targets;
@@ -597,6 +599,8 @@ size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool n
     w.emax = std::min(k, m);
     // stage A over all m rows (compile-time or tile kernels), position tables, snippet stage B
     w.fixed = (sh::has_fixed(k, m, B) || tile_usable(ctx(), k, m, B)) && sh::stageb_fixed_ok(geo, w.emax);
+    const int kfix = force_tile() ? 0 : sh::fixed_kernel_k(k, m, B);
+    w.kp = round4(std::max(k, kfix));
     w.small = w.fixed && sh::stageb_small_ok(geo, w.emax);
     w.ldA = w.fixed ? 0 : round4(k);
     w.ldB = (w.emax + 7) & ~7;  // stage-B coefficients [i][ldB] (transposed, 8-entry rows)
@@ -620,7 +624,7 @@ size_t carve(DecodeWS &w, uint8_t *base, int k, int m, int B, int groups, bool n
                     ? reinterpret_cast<uint64_t *>(take(G * w.emax * w.ldB * sizeof(uint64_t)))
                     : nullptr;
     w.rrow = w.fixed ? take(G * round4(w.emax)) : nullptr;
-    w.pos = w.fixed ? take(G * round4(k)) : nullptr;
+    w.pos = w.fixed ? take(G * w.kp) : nullptr;
     w.rpos = w.fixed ? take(G * round4(m)) : nullptr;
     w.residual = take(G * w.nres * static_cast<size_t>(B) + 256);  // + slack: word over-read
     w.recovered = need_recovered ? take(G * w.emax * static_cast<size_t>(B)) : nullptr;
@@ -746,6 +750,7 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
     sa.coefB_gstride = w.coefB_gs;
     sa.ldB = w.ldB;
     sa.pos = w.pos;
+    sa.kp = w.kp;
     sa.rpos = w.rpos;
     sa.rrow = w.rrow;
     sa.ldR = round4(w.emax);
@@ -775,7 +780,9 @@ int decode_core(Context &c, int k, int m, int B, int groups, const uint8_t *d_bl
     if (w.fixed) {
         // Stage A (compile-time generator, all m rows, erased columns read as zeros):
         //   residual_y = R_y + sum_{received x} M(C[y][x]) d_x
-        const bool sliced = slice_scratch && groups == 1 && tile_usable(c, k, m, B) && latency_slices(k + m) > 1;
+        // (the tile kernels read position tables round4(k) wide: not after a wider compiled K)
+        const bool sliced = slice_scratch && groups == 1 && tile_usable(c, k, m, B) && latency_slices(k + m) > 1 &&
+                            w.kp == round4(k);
         if (sh::has_fixed(k, m, B) && !force_tile() && !sliced) {
             SplitLease sp;
             const bool split = kSplitLaunch && groups >= kSplitMinGroups;
@@ -842,7 +849,7 @@ bool host_decode_setup(const DecodeWS &w, int k, int m, const uint8_t *rows, int
     sh::cauchy_params(k, m, xp, yp);
     *w.e = e;
     std::memset(w.rrow, 0, round4(w.emax));
-    std::memset(w.pos, 0xFF, round4(k));
+    std::memset(w.pos, 0xFF, w.kp);
     std::memset(w.rpos, 0xFF, round4(m));
     for (int j = 0; j < k; ++j) {
         if (rows[j] < k) w.pos[rows[j]] = static_cast<uint8_t>(j);

@@ -201,8 +201,13 @@ struct Src {
     int lgl;                  // ... and its group (position-table index)
     // encode: byte offset of step 0's block (the second half of a split tile starts at block x0)
     mutable uint32_t boff = 0;
-    __device__ __forceinline__ void set_step0(int x0) const { boff = static_cast<uint32_t>(x0) * B; }
+    mutable int x0s = 0;
+    __device__ __forceinline__ void set_step0(int x0) const {
+        boff = static_cast<uint32_t>(x0) * B;
+        x0s = x0;
+    }
     int pf_stride = 0;        // FixedArgs::pf_stride (l2_prefetch)
+    int krt = S::K;           // encode: steps x >= krt (FixedArgs::k_rt) read zeros
 
     __device__ __forceinline__ static void chunk_src(const Geometry &geo, long long in_gstride_, const WGInfo &w,
                                                      uint32_t (&db)[S::DPW], int (&gl)[S::DPW]) {
@@ -240,6 +245,7 @@ struct Src {
         rpos_g = a.rpos;
         lgl = w.gl;
         pf_stride = a.pf_stride;
+        krt = a.k_rt > 0 ? a.k_rt : S::K;
         lbase = w.valid ? static_cast<uint32_t>(w.gl) * static_cast<uint32_t>(a.in_gstride) + col_off(w.q, geo) : OOR;
     }
 
@@ -333,7 +339,7 @@ struct Src {
                     const uint32_t o = (p == 0xFF || ndbase[j] == OOR) ? OOR : ndbase[j] + static_cast<uint32_t>(p) * B;
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(nrsrc, dst, S::W, o, 0, 0, SH_LOAD_AUX);
                 } else {
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(nrsrc, dst, S::W, ndbase[j],
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(nrsrc, dst, S::W, t < krt ? ndbase[j] : OOR,
                                                              static_cast<uint32_t>(t) * B, 0, SH_LOAD_AUX);
                 }
             }
@@ -449,7 +455,7 @@ struct Src {
                 const uint32_t o = (p == 0xFF || dbase[j] == OOR) ? OOR : dbase[j] + static_cast<uint32_t>(p) * B;
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, S::W, o, 0, 0, SH_LOAD_AUX);
             } else {
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, S::W, dbase[j],
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, S::W, x + x0s < krt ? dbase[j] : OOR,
                                                          static_cast<uint32_t>(x) * B + boff, 0, SH_LOAD_AUX);
             }
         }
@@ -1087,6 +1093,8 @@ template <class S, bool DEC, bool STREAM = false, bool PERS = false, bool SPLIT 
 inline hipError_t launch_shape(FixedArgs a, hipStream_t s, void (*kern)(FixedArgs), const char *tag = nullptr,
                                int ntiles = -1) {
     constexpr bool dec = DEC;
+    // a runtime k below K: only the product source (Src) reads zeros past k
+    if (a.k_rt > 0 && a.k_rt != S::K && (STREAM || S::SLOT != S::IMG)) return hipErrorNotSupported;
     a.groups_per_wg = (S::COLS - 1) / a.geo.nq + 2;
     // ring (the row images of the epilogue alias it); a streaming source needs only the images
     constexpr size_t front = STREAM ? 2ull * S::PW * S::SLOT : static_cast<size_t>(S::R) * S::SLOT;

@@ -73,20 +73,31 @@ bool tag_is_module(const char *tag) {
 }
 }  // namespace fixed
 
-bool has_fixed(int k, int m, int B) {
+// A kernel compiled for (K, m) also codes k < K: the generator's column x is the same for every k
+// (cauchy_256.cpp:423-481), and the steps past k read zeros. Those steps still run their XOR
+// programs, so the kernel is used down to k = 0.6 K: at 6,000 groups of 1400 bytes the (224,32)
+// kernel's full 224 steps took 0.585 ms against 0.674 for the tile kernel at (150,32), (200,56)
+// 0.85 vs 1.25 at (150,56), (190,66) 0.98 vs 1.50 at (120,66) (profiles/r06/ab_runs.txt block 13).
+int fixed_kernel_k(int k, int m, int B) {
     // the shifted last 16-byte chunk must stay inside its sub-block (B/8 >= 16; fixed_geometry)
-    if (B % 8 != 0 || B / 8 < 16) return false;
-#define SH_HAS(K, M) if (k == K && m == M) return true;
-    SH_FIXED_CONFIGS(SH_HAS)
-#undef SH_HAS
-    return false;
+    if (B % 8 != 0 || B / 8 < 16 || k < 1) return 0;
+    int best = 0;
+#define SH_FIT(K, M) \
+    if (m == M && k <= K && (k == K || 10 * k >= 6 * K) && (best == 0 || K < best)) best = K;
+    SH_FIXED_CONFIGS(SH_FIT)
+#undef SH_FIT
+    return best;
 }
 
+bool has_fixed(int k, int m, int B) { return fixed_kernel_k(k, m, B) > 0; }
+
 hipError_t launch_fixed(int k, int m, FixedArgs a, bool dec, hipStream_t stream) {
-    if (!has_fixed(k, m, a.geo.B)) return hipErrorNotSupported;
+    const int kk = fixed_kernel_k(k, m, a.geo.B);
+    if (kk == 0) return hipErrorNotSupported;
     if (a.groups <= 0) return hipSuccess;
+    a.k_rt = k;
 #define SH_GO(K, M)                                                                         \
-    if (k == K && m == M)                                                                   \
+    if (kk == K && m == M)                                                                  \
         return dec ? fixed::launch_k##K##_m##M##_dec(a, stream) : fixed::launch_k##K##_m##M##_enc(a, stream);
     SH_FIXED_CONFIGS(SH_GO)
 #undef SH_GO

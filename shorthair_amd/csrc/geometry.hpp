@@ -60,6 +60,11 @@ struct FixedArgs {
     int split_max;            // counters available (split tiles at most)
     int nsplit;
     int pf_stride;            // workgroup slots of the launch (L2 prefetch of a later tile, A/B)
+    // Runtime k (0 = the kernel's compile-time K). For m >= 7 and for the searched m <= 6 tables the
+    // generator's column x does not depend on k (cauchy_256.cpp:423-481), so a kernel compiled for
+    // (K, m) codes any k <= K: its steps x >= k read zeros (encode: out-of-range DMA; decode: the
+    // position tables, K wide, mark them erased).
+    int k_rt;
 };
 
 }  // namespace sh

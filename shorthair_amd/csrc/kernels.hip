@@ -345,7 +345,7 @@ __global__ __launch_bounds__(64 * W, 8) void decode_setup(DecodeSetupArgs a, int
     if (lane == 0) a.e_out[g] = e;
     const bool fixed_mode = (a.coefA == nullptr);
     if (fixed_mode) {
-        const int KP = (k + 3) & ~3, MP = (m + 3) & ~3;
+        const int KP = a.kp, MP = (m + 3) & ~3;
         uint8_t *pos = a.pos + static_cast<long long>(g) * KP;
         uint8_t *rpos = a.rpos + static_cast<long long>(g) * MP;
         for (int x = lane; x < KP; x += 64) pos[x] = 0xFF;
@@ -631,7 +631,7 @@ __device__ int group_prologue(const DecodeSetupArgs &a, int g, int l, int gb, GS
         nera += __popc(me);
     }
     // position tables, assembled in LDS and stored as dwords
-    const int KP = (k + 3) & ~3, MP = (m + 3) & ~3;
+    const int KP = a.kp, MP = (m + 3) & ~3;
     for (int x = l; x < KP; x += L) S.pos[x] = 0xFF;
     for (int y = l; y < MP; y += L) S.rpos[y] = 0xFF;
     SH_WAVE_SYNC();

@@ -49,7 +49,8 @@ struct DecodeSetupArgs {
     // Fixed-kernel mode (coefA == nullptr): stage A runs the compile-time generator over all m
     // rows, so the setup emits position tables instead of stage-A coefficients, and stage B gets
     // the residual row of each received recovery block plus ready-made snippet addresses.
-    uint8_t *pos;           // [G][round4(k)] array index of original row x (0xFF = erased)
+    uint8_t *pos;           // [G][kp] array index of original row x (0xFF = erased, and x >= k)
+    int kp;                 // position-table stride: round4 of the stage-A kernel's K (>= k)
     uint8_t *rpos;          // [G][round4(m)] array index of recovery row y (0xFF = absent)
     uint8_t *rrow;          // [G][ldR] generator row r_i of the i-th received recovery block
     int ldR;                // round4(emax)
@@ -190,6 +191,9 @@ hipError_t launch_tile(const TileArgs &t, bool dec, hipStream_t stream);
 // block is too short (sub < 4).
 hipError_t launch_fixed(int k, int m, FixedArgs a, bool dec, hipStream_t stream);
 bool has_fixed(int k, int m, int B);
+// K of the compile-time kernel that codes (k, m, B): k itself, or the smallest compiled K > k for
+// the same m with k >= 0.6 K (its steps past k read zeros, FixedArgs::k_rt); 0 = none.
+int fixed_kernel_k(int k, int m, int B);
 
 hipError_t launch_apply(const ApplyArgs &a, bool per_group, hipStream_t stream);
 hipError_t launch_xor_rows(const uint8_t *in, long long in_gstride, int n_in, uint8_t *out,

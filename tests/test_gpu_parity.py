@@ -112,7 +112,9 @@ def test_single_group_decode_abi(sh, c):
 # 520 are no compile-time shape (tile kernels), B = 96 is below the tile kernels (generic path).
 @pytest.mark.parametrize("k,m,B", [(200, 32, 1400), (64, 16, 1400), (150, 40, 1352), (28, 8, 256),
                                    (100, 20, 512), (190, 66, 1336), (12, 7, 64),
-                                   (20, 2, 1400), (28, 4, 256), (40, 6, 1000), (30, 4, 96), (17, 5, 520)])
+                                   (20, 2, 1400), (28, 4, 256), (40, 6, 1000), (30, 4, 96), (17, 5, 520),
+                                   # k below a compiled K of the same m (fixed_kernel_k)
+                                   (150, 32, 1400), (20, 4, 256), (130, 56, 1352)])
 def test_single_group_decode_random_patterns(sh, k, m, B):
     """cauchy_256_decode (host-side setup for m >= 7) on random erasure sets: e = 1..min(k, m) lost
     originals, a random subset of e recovery rows, blocks in random array order; results and rows
@@ -196,7 +198,12 @@ def _oracle_encode_groups(k, m, B, cfg, groups):
 
 @pytest.mark.parametrize("k,m,B,G", [(64, 16, 1400, 4096), (28, 4, 256, 512), (112, 16, 1400, 300),
                                      (224, 32, 65536, 8), (200, 32, 1400, 1024), (2, 2, 8, 1000),
-                                     (250, 6, 16, 64), (13, 9, 24, 333)])
+                                     (250, 6, 16, 64), (13, 9, 24, 333),
+                                     # k below a compiled K of the same m: the kernel's steps past
+                                     # k read zeros (fixed_kernel_k)
+                                     (150, 32, 1400, 300), (100, 16, 1400, 300), (20, 4, 1400, 500),
+                                     (150, 56, 1352, 100), (120, 66, 1336, 100), (40, 16, 264, 700),
+                                     (135, 32, 256, 900)])
 def test_encode_batch_vs_oracle(sh, k, m, B, G):
     """BASELINE configs[1] (4096 x k=64 m=16 1400B) and sweep shapes: device-generated input
     equals the oracle's generator (sha of a sample), encode bit-exact on sampled groups."""
@@ -260,7 +267,11 @@ def _decode_inputs(k, m, B, G, cfg, e_fixed):
                                              # nq = 4 / 8 / 12 / 16 word columns, shifted chunks)
                                              (28, 4, 128, 3001, 0), (224, 32, 256, 601, 0),
                                              (112, 16, 384, 333, 16), (200, 32, 136, 257, 0),
-                                             (200, 56, 512, 129, 0), (64, 16, 264, 77, 0)])
+                                             (200, 56, 512, 129, 0), (64, 16, 264, 77, 0),
+                                             # k below a compiled K of the same m
+                                             (150, 32, 1400, 500, 0), (100, 16, 1400, 500, 16),
+                                             (20, 4, 256, 3000, 0), (150, 56, 1352, 200, 0),
+                                             (120, 66, 1336, 200, 0), (40, 16, 256, 2000, 0)])
 def test_decode_batch_roundtrip_and_oracle(sh, k, m, B, G, e_fixed):
     """BASELINE configs[2] (8192 x k=200 m=32 1400B, random erasures up to 32): every group's
     recovered blocks equal the erased originals (encode -> erase -> decode round trip, whole
@@ -483,8 +494,8 @@ def test_searched_table_setup_mixed_groups(sh, k, m, B):
 
 
 @pytest.mark.parametrize("k,m,B", [(50, 10, 1000), (8, 20, 1400), (64, 16, 264), (12, 7, 1400),
-                                   (40, 12, 256), (241, 15, 256), (28, 4, 256), (20, 6, 1400),
-                                   (250, 6, 1400), (40, 2, 512)])
+                                   (40, 12, 256), (241, 15, 256), (100, 16, 256), (28, 4, 256),
+                                   (20, 6, 1400), (20, 4, 1400), (250, 6, 1400), (40, 2, 512)])
 def test_multi_group_setup_mixed_groups_many(sh, k, m, B):
     """More than 8192 groups, where the multi-group setups run (m >= 7 with emax <= 16:
     decode_setup_cauchy, 16 lanes per group; m <= 6: decode_setup_small, 8 lanes per group):
