@@ -416,7 +416,8 @@ SWEEP = [("C2", 64, 16, 1400), ("C2 4096 groups", 64, 16, 1400, 4096)] + [("C4",
                                   for B in (256, 1400, 65536)] + \
         [("tester", 200, 56, 1352), ("tester", 190, 66, 1336), ("tester", 190, 66, 1344)] + \
         [("off-grid", 120, 136, 1400), ("off-grid", 150, 40, 1400), ("off-grid", 50, 10, 1000),
-         ("off-grid", 180, 76, 1352)]
+         ("off-grid", 180, 76, 1352)] + \
+        [("k < K", 150, 32, 1400), ("k < K", 150, 56, 1352), ("k < K", 120, 66, 1336)]  # fixed_kernel_k
 
 
 def sweep(args, sh, torch, s):
