@@ -203,7 +203,7 @@ def _oracle_encode_groups(k, m, B, cfg, groups):
                                      # k read zeros (fixed_kernel_k)
                                      (150, 32, 1400, 300), (100, 16, 1400, 300), (20, 4, 1400, 500),
                                      (150, 56, 1352, 100), (120, 66, 1336, 100), (40, 16, 264, 700),
-                                     (135, 32, 256, 900)])
+                                     (135, 32, 256, 900), (150, 40, 1400, 301), (216, 40, 1400, 64)])
 def test_encode_batch_vs_oracle(sh, k, m, B, G):
     """BASELINE configs[1] (4096 x k=64 m=16 1400B) and sweep shapes: device-generated input
     equals the oracle's generator (sha of a sample), encode bit-exact on sampled groups."""
@@ -271,7 +271,8 @@ def _decode_inputs(k, m, B, G, cfg, e_fixed):
                                              # k below a compiled K of the same m
                                              (150, 32, 1400, 500, 0), (100, 16, 1400, 500, 16),
                                              (20, 4, 256, 3000, 0), (150, 56, 1352, 200, 0),
-                                             (120, 66, 1336, 200, 0), (40, 16, 256, 2000, 0)])
+                                             (120, 66, 1336, 200, 0), (40, 16, 256, 2000, 0),
+                                             (150, 40, 1400, 301, 0), (216, 40, 1400, 64, 40)])
 def test_decode_batch_roundtrip_and_oracle(sh, k, m, B, G, e_fixed):
     """BASELINE configs[2] (8192 x k=200 m=32 1400B, random erasures up to 32): every group's
     recovered blocks equal the erased originals (encode -> erase -> decode round trip, whole
@@ -310,7 +311,7 @@ def test_decode_batch_roundtrip_and_oracle(sh, k, m, B, G, e_fixed):
 # (tile_parts: 1, 2, 4, 6, 8, 12, 16 parts of 4..8 rows; m = 3, 10, 24, 40, 60, 76, 100), two
 # launches (m > 128), the shapes Shorthair's policy issues between the compiled pairs, and odd group
 # counts (partial tiles).
-TILE_SHAPES = [(120, 136, 1400, 37), (150, 40, 1400, 301), (50, 10, 1000, 513), (180, 76, 1352, 45),
+TILE_SHAPES = [(120, 136, 1400, 37), (150, 44, 1400, 301), (50, 10, 1000, 513), (180, 76, 1352, 45),
                (2, 254, 128, 61), (100, 100, 200, 77), (5, 3, 128, 999), (70, 72, 520, 130),
                (17, 5, 1352, 9), (60, 24, 4104, 11), (33, 33, 136, 257), (240, 16, 264, 40),
                (150, 60, 1400, 33), (90, 49, 512, 70)]

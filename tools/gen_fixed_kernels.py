@@ -34,8 +34,10 @@ OUTDIR = os.path.join(ROOT, "shorthair_amd", "csrc", "gen")
 
 # (k, m): BASELINE.json configs -- headline (200,32), C2 (64,16), C4 sweep (28,4),(112,16),(224,32)
 # -- and the shapes catid/shorthair's own caller issues: Shorthair.cpp:502-504 clamps m to 256-k,
-# so its Tester runs k=200/m=56 and k=190/m=66.
-CONFIGS = [(200, 32), (64, 16), (28, 4), (112, 16), (224, 32), (200, 56), (190, 66)]
+# so its Tester runs k=200/m=56 and k=190/m=66. (216, 40) = (256 - m, m): with the
+# k < K dispatch (sh::fixed_kernel_k) it codes every k in [130, 216] of m = 40, the sweep's
+# off-grid (150, 40) included (profiles/r06/ab_runs.txt block 14).
+CONFIGS = [(200, 32), (64, 16), (28, 4), (112, 16), (224, 32), (200, 56), (190, 66), (216, 40)]
 if os.environ.get("SH_CONFIGS"):  # experiments: e.g. SH_CONFIGS="200,32;64,16"
     CONFIGS = [tuple(map(int, c.split(","))) for c in os.environ["SH_CONFIGS"].split(";")]
 ROWS_PER_PART = int(os.environ.get("SH_ROWS_PER_PART", "8"))
