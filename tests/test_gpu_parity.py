@@ -114,7 +114,7 @@ def test_single_group_decode_abi(sh, c):
                                    (100, 20, 512), (190, 66, 1336), (12, 7, 64),
                                    (20, 2, 1400), (28, 4, 256), (40, 6, 1000), (30, 4, 96), (17, 5, 520),
                                    # k below a compiled K of the same m (fixed_kernel_k)
-                                   (150, 32, 1400), (20, 4, 256), (130, 56, 1352)])
+                                   (150, 32, 1400), (20, 4, 256), (130, 56, 1352), (150, 40, 1400)])
 def test_single_group_decode_random_patterns(sh, k, m, B):
     """cauchy_256_decode (host-side setup for m >= 7) on random erasure sets: e = 1..min(k, m) lost
     originals, a random subset of e recovery rows, blocks in random array order; results and rows
