@@ -76,7 +76,8 @@ int cauchy_256_fill_synthetic(void *d_out, int n, int block_bytes, int groups,
 int cauchy_256_erasure_pattern(unsigned long long g, int k, int m, unsigned long long cfg, int e_fixed,
                                unsigned char *rows_out);
 
-/* Which kernels code (k, m, block_bytes): 1 = compile-time-scheduled (generated for this (k, m)),
+/* Which kernels code (k, m, block_bytes): 1 = compile-time-scheduled (generated for this (k, m), or
+ * for a larger K of the same m with k >= 0.6 K, whose steps past k then read zeros),
  * 2 = the runtime-coefficient tile kernels (any other (k, m) with block_bytes/8 >= 16),
  * 0 = the generic per-column kernels (shorter blocks), -1 = invalid parameters. Host-only: never
  * initialises the GPU. Before the library is initialised, 2 assumes the snippet table loaded
